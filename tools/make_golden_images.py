@@ -1,0 +1,29 @@
+"""Build the real-image fixtures from the reference's own test data.
+
+The reference test (test/gpu_detector_test.cu:40-47) does
+imread(colorimage.jpg) -> cvtColor(BGR2YUV_YUYV) -> GpuDetector::Detect.
+OpenCV is absent offline, so the JPEG is decoded once here with PIL and the
+Y plane is computed with OpenCV's BT.601 fixed-point formula (the one the
+YUYV conversion uses, ITUR_BT_601_SHIFT = 20).  The result is committed as a
+lossless PNG so JPEG-decoder differences can never move the fixture.
+Reads /root/reference at generation time only.
+"""
+import numpy as np
+from PIL import Image
+
+SRC = "/root/reference/src/apriltags_cuda/test/data/"
+DST = "/root/repo/tests/golden/"
+
+
+def y_bt601(rgb: np.ndarray) -> np.ndarray:
+    r = rgb[..., 0].astype(np.int64)
+    g = rgb[..., 1].astype(np.int64)
+    b = rgb[..., 2].astype(np.int64)
+    y = (269484 * r + 528482 * g + 102760 * b + (1 << 19) + (16 << 20)) >> 20
+    return y.astype(np.uint8)
+
+
+for name in ["colorimage", "colorimage_notags"]:
+    rgb = np.asarray(Image.open(SRC + name + ".jpg").convert("RGB"))
+    Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
+    print(name, rgb.shape)
