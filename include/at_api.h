@@ -1,0 +1,147 @@
+/*
+ * at_api.h -- C ABI of the MI355X-native AprilTag detection stage.
+ *
+ * Drop-in boundary for the reference's per-frame detector
+ * frc971::apriltag::GpuDetector (Team766/ros_vision,
+ * src/apriltags_cuda/include/apriltags_cuda/apriltag_gpu.h:77-359), whose
+ * caller is ApriltagsDetector::imageCallback
+ * (src/apriltags_cuda/src/apriltags_cuda_detector.cu:382-557).  Plain C types
+ * only; every entry point returns 0 or a negative AT_E* code (the reference
+ * aborts through glog CHECK instead, cuda_frc971.h:14-17).
+ *
+ * Threading: one at_detector per camera stream (the reference owns one
+ * GpuDetector + one CUDA stream per node, apriltag_gpu.h:240); calls on one
+ * instance must not overlap.
+ */
+#ifndef AT_API_H_
+#define AT_API_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AT_ABI_VERSION 1
+
+enum {
+  AT_OK = 0,
+  AT_E_INVALID = -1,    /* bad argument / unsupported geometry */
+  AT_E_HIP = -2,        /* HIP runtime error (no device, launch failure) */
+  AT_E_CAPACITY = -3,   /* frame exceeded a fixed capacity (see at_frame_status) */
+  AT_E_FAMILY = -4,     /* unknown tag family */
+  AT_E_NOMEM = -5
+};
+
+typedef struct at_detector at_detector; /* opaque: device buffers + hipStream_t */
+
+typedef enum { AT_FMT_YUYV = 0, AT_FMT_BGR8 = 1, AT_FMT_GRAY8 = 2 } at_pixfmt;
+
+/* CameraMatrix + DistCoeffs (apriltag_gpu.h:61-74), read from
+ * calibrationmatrix_<serial>.json by apriltags_cuda_detector.cu:315-371. */
+typedef struct {
+  double fx, fy, cx, cy;
+  double k1, k2, p1, p2, k3;
+} at_camera;
+
+/* apriltag_detector_t fields the reference consults
+ * (apriltags_cuda_detector.cu:139-147; apriltag_gpu.cu:166-181, 737, 884, 1084-1086). */
+typedef struct {
+  int width, height;          /* frame size; width%8==0, height%8==0, width*height < 2^22 */
+  const char *family;         /* "tag36h11" (apriltags_cuda_detector.hpp:213) */
+  float quad_decimate;        /* must be 2.0 (apriltag_gpu.cu:166) */
+  int refine_edges;           /* 1 */
+  double decode_sharpening;   /* 0.25 */
+  int min_white_black_diff;   /* 5 */
+  int min_cluster_pixels;     /* 5 */
+  int max_nmaxima;            /* must be 10 (line_fit_filter.cu:1205) */
+  float max_line_fit_mse;     /* 10.0 */
+  double cos_critical_rad;    /* cos(10 deg) */
+  int device;                 /* HIP device ordinal */
+  int max_batch;              /* frames per at_detect_batch / at_detect_device call */
+} at_config;
+
+/* apriltag_detection_t fields published downstream (apriltag.h; consumed at
+ * apriltags_cuda_detector.cu:425-496). */
+typedef struct {
+  int32_t id;
+  int32_t hamming;
+  float decision_margin;
+  double H[9];      /* row-major 3x3 homography, tag [-1,1]^2 -> pixels */
+  double c[2];      /* centre */
+  double p[4][2];   /* corners */
+} at_detection;
+
+/* Fills the reference defaults for a width x height camera. */
+int at_config_default(at_config *cfg, int width, int height);
+
+/* GpuDetector::GpuDetector (apriltag_gpu.cu:111-188): allocates every buffer
+ * at worst-case size for max_batch frames; nothing is allocated per frame. */
+int at_create(const at_config *cfg, const at_camera *cam, at_detector **out);
+
+/* GpuDetector::Detect + Detections (apriltag_gpu.cu:725-1166,
+ * apriltag_detect.cu:618-663): one host frame in, detections sorted by id out.
+ * *n receives the total found; at most cap are written. Synchronous. */
+int at_detect(at_detector *d, const uint8_t *frame, at_pixfmt fmt, at_detection *out, int cap, int *n);
+
+/* Batched host frames (one launch sequence for all frames; multi-camera). */
+int at_detect_batch(at_detector *d, const uint8_t *const *frames, int nframes, at_pixfmt fmt,
+                    at_detection *out, int cap_per_frame, int *n_per_frame);
+
+/* Frames already resident in device memory: d_frames is a device pointer to
+ * nframes frames laid out back to back (frame_stride bytes apart). */
+int at_detect_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt,
+                     at_detection *out, int cap_per_frame, int *n_per_frame);
+
+/* Split-phase form of at_detect_device for pipelining: enqueue the batch on
+ * the detector's stream and return immediately; at_collect waits for it and
+ * runs the host tail (reconcile + sort by id). */
+int at_enqueue_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt);
+int at_collect(at_detector *d, at_detection *out, int cap_per_frame, int *n_per_frame);
+
+/* Per-frame status of the last batch: 0 or AT_E_CAPACITY (a frame whose blob
+ * pair count exceeded the reference's 12-bit blob index, points.h:183-193). */
+int at_frame_status(at_detector *d, int frame);
+
+/* Per-stage parity taps (the reference's Copy*To debug accessors,
+ * apriltag_gpu.h:98-183).  Copies the named stage of frame `frame` of the
+ * last batch into dst (host memory). Returns bytes copied or < 0. */
+enum {
+  AT_STAGE_GRAY = 0,        /* u8  [H][W] */
+  AT_STAGE_DECIMATED = 1,   /* u8  [H/2][W/2] */
+  AT_STAGE_THRESHOLD = 2,   /* u8  [H/2][W/2] in {0,127,255} */
+  AT_STAGE_LABELS = 3,      /* u32 [H/2][W/2] */
+  AT_STAGE_SIZES = 4,       /* u32 [H/2 * W/2] */
+  AT_STAGE_NUM_POINTS = 5,  /* u32 count of boundary points N_c */
+  AT_STAGE_NUM_PAIRS = 6,   /* u32 count of blob pairs N_q */
+  AT_STAGE_QUADS = 7,       /* at_quad_record[] of fitted quads (see below) */
+  AT_STAGE_POINTS = 8,      /* u64 QuadBoundaryPoint keys, grouped by pair rank */
+  AT_STAGE_BLOB_POINTS = 9  /* u64 IndexPoint keys of selected blobs, sorted (blob, theta) */
+};
+long long at_debug_copy(at_detector *d, int stage, int frame, void *dst, size_t bytes);
+
+/* Fitted quad record (FitQuad + QuadCorners, line_fit_filter.h:130-135 and
+ * apriltag_gpu.h:55-59). */
+typedef struct {
+  uint32_t blob_index;
+  uint32_t valid;          /* FitQuads valid flag */
+  uint32_t accepted;       /* passed UpdateFitQuads checks */
+  uint16_t indices[4];
+  float corners[4][2];     /* after AdjustPixelCenters (full resolution) */
+} at_quad_record;
+
+void at_destroy(at_detector *d);
+const char *at_strerror(int code);
+
+/* Family data (host only, no device needed). */
+int at_family_num_known(const char *family);
+int at_family_entry(const char *family, int i, int *id, uint64_t *code);
+
+/* Library self-description. */
+int at_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AT_API_H_ */

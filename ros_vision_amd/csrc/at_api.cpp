@@ -1,0 +1,504 @@
+// at_api.cpp -- host side of the C ABI (include/at_api.h).
+//
+// Owns the device buffers (sized once, for max_batch frames at worst case,
+// like GpuDetector's constructor, apriltag_gpu.cu:111-188), launches the
+// kernel pipeline on one HIP stream and runs the small host tail: order the
+// per-frame candidates by blob rank (the reference decodes quads in blob-index
+// order, apriltag_detect.cu:642-658), reconcile_detections and zarray_sort by
+// id (apriltag_detect.cu:660-662).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/at_api.h"
+#include "at_common.h"
+
+namespace at {
+hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
+hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
+                           hipStream_t st);
+
+struct CodeEntry {
+  int id;
+  uint64_t code;
+};
+static const CodeEntry kTag36h11[] = {
+#include "at_tag36h11_codes.inc"
+};
+static const int kTag36h11Known = (int)(sizeof(kTag36h11) / sizeof(kTag36h11[0]));
+}  // namespace at
+
+using namespace at;
+
+struct at_detector {
+  at_config cfg;
+  at_camera cam;
+  Geom g;
+  Params prm;
+  int B;
+  int device;
+  int nblobwg;
+  hipStream_t st;
+  DevBufs d;
+  std::vector<void*> allocs;
+  uint8_t* d_in;            // staging for host frames [B][max frame bytes]
+  size_t in_stride;
+  const uint8_t** d_ftab;   // device frame pointer table
+  const uint8_t** h_ftab;   // pinned
+  uint32_t* d_ctrl;         // control block (zeroed each batch)
+  size_t ctrl_words;
+  uint32_t* h_ctrl;         // pinned copy of the control block
+  DevDetection* h_dets;     // pinned [B][kMaxDets]
+  int last_nframes;
+  int pending;
+  hipEvent_t ev_done;
+};
+
+static int hip_fail(hipError_t e) {
+  if (e != hipSuccess) {
+    fprintf(stderr, "at_api: HIP error %s\n", hipGetErrorString(e));
+    return AT_E_HIP;
+  }
+  return AT_OK;
+}
+#define HIPCHK(x)                          \
+  do {                                     \
+    hipError_t e_ = (x);                   \
+    if (e_ != hipSuccess) return hip_fail(e_); \
+  } while (0)
+
+extern "C" {
+
+int at_abi_version(void) { return AT_ABI_VERSION; }
+
+const char* at_strerror(int code) {
+  switch (code) {
+    case AT_OK: return "ok";
+    case AT_E_INVALID: return "invalid argument or unsupported frame geometry";
+    case AT_E_HIP: return "HIP runtime error";
+    case AT_E_CAPACITY: return "frame exceeded a fixed capacity";
+    case AT_E_FAMILY: return "unknown tag family";
+    case AT_E_NOMEM: return "out of memory";
+    default: return "unknown error";
+  }
+}
+
+int at_family_num_known(const char* family) {
+  if (!family || strcmp(family, "tag36h11") != 0) return AT_E_FAMILY;
+  return kTag36h11Known;
+}
+
+int at_family_entry(const char* family, int i, int* id, uint64_t* code) {
+  if (!family || strcmp(family, "tag36h11") != 0) return AT_E_FAMILY;
+  if (i < 0 || i >= kTag36h11Known) return AT_E_INVALID;
+  if (id) *id = kTag36h11[i].id;
+  if (code) *code = kTag36h11[i].code;
+  return AT_OK;
+}
+
+int at_config_default(at_config* cfg, int width, int height) {
+  if (!cfg) return AT_E_INVALID;
+  memset(cfg, 0, sizeof(*cfg));
+  cfg->width = width;
+  cfg->height = height;
+  cfg->family = "tag36h11";
+  cfg->quad_decimate = 2.0f;
+  cfg->refine_edges = 1;
+  cfg->decode_sharpening = 0.25;
+  cfg->min_white_black_diff = 5;
+  cfg->min_cluster_pixels = 5;
+  cfg->max_nmaxima = 10;
+  cfg->max_line_fit_mse = 10.0f;
+  cfg->cos_critical_rad = cos(10.0 * M_PI / 180.0);
+  cfg->device = 0;
+  cfg->max_batch = 1;
+  return AT_OK;
+}
+
+void at_destroy(at_detector* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  if (d->st) (void)hipStreamSynchronize(d->st);
+  for (void* p : d->allocs) (void)hipFree(p);
+  if (d->h_ftab) (void)hipHostFree(d->h_ftab);
+  if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
+  if (d->h_dets) (void)hipHostFree(d->h_dets);
+  if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+  if (d->st) (void)hipStreamDestroy(d->st);
+  delete d;
+}
+
+int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
+  if (!cfg || !cam || !out) return AT_E_INVALID;
+  *out = nullptr;
+  if (!cfg->family || strcmp(cfg->family, "tag36h11") != 0) return AT_E_FAMILY;
+  const int W = cfg->width, H = cfg->height;
+  // GpuDetector preconditions (apriltag_gpu.cu:166-167, 754-755, 774; line_fit_filter.cu:1205)
+  if (W <= 16 || H <= 16 || W % 8 || H % 8 || (long)W * H >= (1L << 22)) return AT_E_INVALID;
+  if (cfg->quad_decimate != 2.0f || cfg->max_nmaxima != 10 || cfg->max_batch < 1) return AT_E_INVALID;
+  if (2 * (W + H) > kSortCap) return AT_E_INVALID;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AT_E_HIP;
+  at_detector* d = new at_detector();  // value-initialised: every pointer null
+  d->cfg = *cfg;
+  d->cfg.family = "tag36h11";
+  d->cam = *cam;
+  d->device = cfg->device;
+  d->B = cfg->max_batch;
+  Geom& g = d->g;
+  g.W = W; g.H = H; g.Wd = W / 2; g.Hd = H / 2;
+  g.TW = g.Wd / 4; g.TH = g.Hd / 4;
+  g.BW = g.Wd / 2; g.BH = g.Hd / 2;
+  g.CTX = (g.Wd + kCclTile - 1) / kCclTile;
+  g.CTY = (g.Hd + kCclTile - 1) / kCclTile;
+  g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
+  g.min_cluster = (uint32_t)std::max(24, cfg->min_cluster_pixels);
+  g.max_cluster = (uint32_t)(2 * (W + H));
+  g.min_tag_width = std::max(3, 8 / 2);  // tag36h11 width_at_border 8 / quad_decimate 2
+  Params& p = d->prm;
+  p.min_white_black_diff = cfg->min_white_black_diff;
+  p.max_line_fit_mse = cfg->max_line_fit_mse;
+  p.cos_critical_rad = cfg->cos_critical_rad;
+  p.decode_sharpening = cfg->decode_sharpening;
+  p.refine_edges = cfg->refine_edges;
+  p.fx = cam->fx; p.fy = cam->fy; p.cx = cam->cx; p.cy = cam->cy;
+  p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
+
+  auto fail = [&](int code) {
+    at_destroy(d);
+    return code;
+  };
+  if (hipSetDevice(d->device) != hipSuccess) return fail(AT_E_HIP);
+  if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
+  if (hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
+  int ncu = 0;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
+  d->nblobwg = std::max(64, ncu * 2);
+
+  const size_t B = (size_t)d->B;
+  const size_t npix = (size_t)W * H, nd = (size_t)g.Wd * g.Hd, nt = (size_t)g.TW * g.TH * 2;
+  bool oom = false;
+  auto dalloc = [&](size_t bytes) -> void* {
+    void* ptr = nullptr;
+    if (hipMalloc(&ptr, std::max<size_t>(bytes, 256)) != hipSuccess) {
+      oom = true;
+      return nullptr;
+    }
+    d->allocs.push_back(ptr);
+    return ptr;
+  };
+  d->in_stride = (npix * 3 + 255) & ~(size_t)255;
+  d->d_in = (uint8_t*)dalloc(B * d->in_stride);
+  d->d_ftab = (const uint8_t**)dalloc(B * sizeof(void*));
+  DevBufs& b = d->d;
+  b.frames = d->d_ftab;
+  b.gray = (uint8_t*)dalloc(B * npix);
+  b.dec = (uint8_t*)dalloc(B * nd);
+  b.mm = (uint8_t*)dalloc(B * nt);
+  b.thr = (uint8_t*)dalloc(B * nd);
+  b.par = (uint32_t*)dalloc(B * nd * 4);
+  b.lab = (uint32_t*)dalloc(B * nd * 4);
+  b.size = (uint32_t*)dalloc(B * nd * 4);
+  b.pts = (uint64_t*)dalloc(B * g.cap_pts * 8);
+  b.grp = (uint64_t*)dalloc(B * g.cap_pts * 8);
+  b.ht_key = (uint64_t*)dalloc(B * kHashSlots * 8);
+  b.ht_cnt = (uint32_t*)dalloc(B * kHashSlots * 4);
+  b.ht_rank = (uint32_t*)dalloc(B * kHashSlots * 4);
+  b.ht_off = (uint32_t*)dalloc(B * kHashSlots * 4);
+  b.ht_cur = (uint32_t*)dalloc(B * kHashSlots * 4);
+  b.pair_cnt = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.pair_off = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.pair_sel = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.work = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
+  b.quads = (QuadRecord*)dalloc(B * kMaxQuads * sizeof(QuadRecord));
+  d->ctrl_words = 5 * B + 2;
+  d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
+  b.npts = d->d_ctrl;
+  b.npairs = d->d_ctrl + B;
+  b.ndets = d->d_ctrl + 2 * B;
+  b.nquads = d->d_ctrl + 3 * B;
+  b.status = d->d_ctrl + 4 * B;
+  b.nwork = d->d_ctrl + 5 * B;
+  b.workhead = d->d_ctrl + 5 * B + 1;
+  const size_t nw = (size_t)d->nblobwg;
+  b.s_i32 = (int32_t*)dalloc(nw * 3 * kSortCap * 4);
+  b.s_i64 = (int64_t*)dalloc(nw * 3 * kSortCap * 8);
+  b.s_f64 = (double*)dalloc(nw * 2 * kSortCap * 8);
+  if (oom) return fail(AT_E_NOMEM);
+  if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
+  if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
+  if (hipHostMalloc((void**)&d->h_dets, B * kMaxDets * sizeof(DevDetection), hipHostMallocDefault) != hipSuccess)
+    return fail(AT_E_NOMEM);
+  {
+    std::vector<uint64_t> codes(kTag36h11Known);
+    std::vector<int> ids(kTag36h11Known);
+    for (int i = 0; i < kTag36h11Known; i++) {
+      codes[i] = kTag36h11[i].code;
+      ids[i] = kTag36h11[i].id;
+    }
+    if (upload_codebook(codes.data(), ids.data(), kTag36h11Known) != hipSuccess) return fail(AT_E_HIP);
+  }
+  // size arrays are read for every label by k_boundary: start defined
+  if (hipMemsetAsync(b.size, 0, B * nd * 4, d->st) != hipSuccess) return fail(AT_E_HIP);
+  if (hipStreamSynchronize(d->st) != hipSuccess) return fail(AT_E_HIP);
+  *out = d;
+  return AT_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// host tail: reconcile_detections + zarray_sort (apriltag 3.x apriltag.c,
+// called at apriltag_detect.cu:660-662)
+// ---------------------------------------------------------------------------
+static bool seg_intersect(const double* a0, const double* a1, const double* b0, const double* b1) {
+  const double ux = a1[0] - a0[0], uy = a1[1] - a0[1];
+  const double vx = b1[0] - b0[0], vy = b1[1] - b0[1];
+  const double den = ux * vy - uy * vx;
+  if (fabs(den) < 1e-12) return false;
+  const double t = ((b0[0] - a0[0]) * vy - (b0[1] - a0[1]) * vx) / den;
+  const double w = ((b0[0] - a0[0]) * uy - (b0[1] - a0[1]) * ux) / den;
+  return t >= 0 && t <= 1 && w >= 0 && w <= 1;
+}
+static bool poly_contains(const double poly[4][2], const double* pt) {
+  bool inside = false;
+  for (int i = 0, j = 3; i < 4; j = i++) {
+    if (((poly[i][1] > pt[1]) != (poly[j][1] > pt[1])) &&
+        (pt[0] < (poly[j][0] - poly[i][0]) * (pt[1] - poly[i][1]) / (poly[j][1] - poly[i][1]) + poly[i][0]))
+      inside = !inside;
+  }
+  return inside;
+}
+static bool poly_overlap(const double a[4][2], const double b[4][2]) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++)
+      if (seg_intersect(a[i], a[(i + 1) & 3], b[j], b[(j + 1) & 3])) return true;
+  return poly_contains(a, b[0]) || poly_contains(b, a[0]);
+}
+static int prefer_smaller(int pref, double q0, double q1) {
+  if (pref) return pref;
+  if (q0 < q1) return -1;
+  if (q1 < q0) return 1;
+  return 0;
+}
+
+static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int cap) {
+  std::vector<DevDetection> v(cand, cand + ncand);
+  std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.blob_rank < b.blob_rank; });
+  int n = (int)v.size();
+  for (int i0 = 0; i0 < n; i0++) {
+    for (int i1 = i0 + 1; i1 < n; i1++) {
+      if (v[i0].id != v[i1].id) continue;
+      if (!poly_overlap(v[i0].p, v[i1].p)) continue;
+      int pref = 0;
+      pref = prefer_smaller(pref, v[i0].hamming, v[i1].hamming);
+      pref = prefer_smaller(pref, -v[i0].decision_margin, -v[i1].decision_margin);
+      for (int k = 0; k < 3; k++) pref = prefer_smaller(pref, v[i0].H[k], v[i1].H[k]);
+      if (pref < 0) {  // keep i0; zarray_remove_index(shuffle=1)
+        if (i1 < n - 1) v[i1] = v[n - 1];
+        n--;
+        i1--;
+      } else {
+        if (i0 < n - 1) v[i0] = v[n - 1];
+        n--;
+        i0--;
+        break;
+      }
+    }
+  }
+  v.resize(n);
+  std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.id < b.id; });
+  for (int i = 0; i < n && i < cap; i++) {
+    at_detection& o = out[i];
+    o.id = v[i].id;
+    o.hamming = v[i].hamming;
+    o.decision_margin = v[i].decision_margin;
+    memcpy(o.H, v[i].H, sizeof(o.H));
+    memcpy(o.c, v[i].c, sizeof(o.c));
+    memcpy(o.p, v[i].p, sizeof(o.p));
+  }
+  return n;
+}
+
+static int enqueue(at_detector* d, int nframes, int fmt) {
+  hipStream_t st = d->st;
+  HIPCHK(hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st));
+  HIPCHK(launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st));
+  HIPCHK(hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(d->ev_done, st));
+  d->last_nframes = nframes;
+  d->pending = 1;
+  return AT_OK;
+}
+
+static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_per_frame) {
+  if (!d->pending) return AT_E_INVALID;
+  HIPCHK(hipEventSynchronize(d->ev_done));
+  d->pending = 0;
+  const int B = d->B;
+  int rc = AT_OK;
+  for (int f = 0; f < d->last_nframes; f++) {
+    const uint32_t status = d->h_ctrl[4 * B + f];
+    const int ncand = (int)std::min<uint32_t>(d->h_ctrl[2 * B + f], (uint32_t)kMaxDets);
+    int n = 0;
+    if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow)) {
+      rc = AT_E_CAPACITY;
+    } else {
+      n = host_tail(d->h_dets + (size_t)f * kMaxDets, ncand, out ? out + (size_t)f * cap_per_frame : nullptr,
+                    out ? cap_per_frame : 0);
+    }
+    if (n_per_frame) n_per_frame[f] = n;
+  }
+  return rc;
+}
+
+static int check_fmt(int fmt) { return fmt == AT_FMT_YUYV || fmt == AT_FMT_BGR8 || fmt == AT_FMT_GRAY8; }
+static size_t frame_bytes(const at_detector* d, int fmt) {
+  const size_t npix = (size_t)d->g.W * d->g.H;
+  return fmt == AT_FMT_YUYV ? 2 * npix : (fmt == AT_FMT_BGR8 ? 3 * npix : npix);
+}
+
+extern "C" {
+
+int at_detect_batch(at_detector* d, const uint8_t* const* frames, int nframes, at_pixfmt fmt, at_detection* out,
+                    int cap_per_frame, int* n_per_frame) {
+  if (!d || !frames || nframes < 1 || nframes > d->B || !check_fmt(fmt)) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  const size_t fb = frame_bytes(d, fmt);
+  for (int f = 0; f < nframes; f++) {
+    HIPCHK(hipMemcpyAsync(d->d_in + (size_t)f * d->in_stride, frames[f], fb, hipMemcpyHostToDevice, d->st));
+    d->h_ftab[f] = d->d_in + (size_t)f * d->in_stride;
+  }
+  int rc = enqueue(d, nframes, fmt);
+  if (rc) return rc;
+  return collect(d, out, cap_per_frame, n_per_frame);
+}
+
+int at_detect(at_detector* d, const uint8_t* frame, at_pixfmt fmt, at_detection* out, int cap, int* n) {
+  const uint8_t* frames[1] = {frame};
+  int nn = 0;
+  const int rc = at_detect_batch(d, frames, 1, fmt, out, cap, &nn);
+  if (n) *n = nn;
+  return rc;
+}
+
+int at_enqueue_device(at_detector* d, const void* d_frames, size_t frame_stride, int nframes, at_pixfmt fmt) {
+  if (!d || !d_frames || nframes < 1 || nframes > d->B || !check_fmt(fmt)) return AT_E_INVALID;
+  if (fmt == AT_FMT_YUYV && frame_stride % 16) return AT_E_INVALID;
+  if (frame_stride % 8) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));  // pinned buffers are reused
+  for (int f = 0; f < nframes; f++) d->h_ftab[f] = (const uint8_t*)d_frames + (size_t)f * frame_stride;
+  return enqueue(d, nframes, fmt);
+}
+
+int at_collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_per_frame) {
+  if (!d) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  return collect(d, out, cap_per_frame, n_per_frame);
+}
+
+int at_detect_device(at_detector* d, const void* d_frames, size_t frame_stride, int nframes, at_pixfmt fmt,
+                     at_detection* out, int cap_per_frame, int* n_per_frame) {
+  int rc = at_enqueue_device(d, d_frames, frame_stride, nframes, fmt);
+  if (rc) return rc;
+  return at_collect(d, out, cap_per_frame, n_per_frame);
+}
+
+int at_frame_status(at_detector* d, int frame) {
+  if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
+  const uint32_t s = d->h_ctrl[4 * d->B + frame];
+  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow)) ? AT_E_CAPACITY : AT_OK;
+}
+
+long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t bytes) {
+  if (!d || !dst || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
+  if (hipSetDevice(d->device) != hipSuccess) return AT_E_HIP;
+  if (d->pending && hipEventSynchronize(d->ev_done) != hipSuccess) return AT_E_HIP;
+  const Geom& g = d->g;
+  const size_t npix = (size_t)g.W * g.H, nd = (size_t)g.Wd * g.Hd;
+  const void* src = nullptr;
+  size_t n = 0;
+  const int B = d->B;
+  std::vector<uint8_t> tmp;
+  switch (stage) {
+    case AT_STAGE_GRAY: src = d->d.gray + frame * npix; n = npix; break;
+    case AT_STAGE_DECIMATED: src = d->d.dec + frame * nd; n = nd; break;
+    case AT_STAGE_THRESHOLD: src = d->d.thr + frame * nd; n = nd; break;
+    case AT_STAGE_LABELS: src = d->d.lab + frame * nd; n = nd * 4; break;
+    case AT_STAGE_SIZES: src = d->d.size + frame * nd; n = nd * 4; break;
+    case AT_STAGE_NUM_POINTS:
+      if (bytes < 4) return AT_E_INVALID;
+      memcpy(dst, &d->h_ctrl[frame], 4);
+      return 4;
+    case AT_STAGE_NUM_PAIRS:
+      if (bytes < 4) return AT_E_INVALID;
+      memcpy(dst, &d->h_ctrl[B + frame], 4);
+      return 4;
+    case AT_STAGE_QUADS: {
+      const uint32_t nq = std::min<uint32_t>(d->h_ctrl[3 * B + frame], (uint32_t)kMaxQuads);
+      std::vector<QuadRecord> q(nq);
+      if (nq && hipMemcpy(q.data(), d->d.quads + (size_t)frame * kMaxQuads, nq * sizeof(QuadRecord),
+                          hipMemcpyDeviceToHost) != hipSuccess)
+        return AT_E_HIP;
+      std::sort(q.begin(), q.end(), [](const QuadRecord& a, const QuadRecord& b) { return a.blob_index < b.blob_index; });
+      const size_t need = nq * sizeof(at_quad_record);
+      if (bytes < need) return AT_E_INVALID;
+      for (uint32_t i = 0; i < nq; i++) {
+        at_quad_record r;
+        r.blob_index = q[i].blob_index;
+        r.valid = q[i].valid;
+        r.accepted = q[i].accepted;
+        memcpy(r.indices, q[i].indices, sizeof(r.indices));
+        memcpy(r.corners, q[i].corners, sizeof(r.corners));
+        memcpy((uint8_t*)dst + i * sizeof(at_quad_record), &r, sizeof(r));
+      }
+      return (long long)need;
+    }
+    case AT_STAGE_POINTS: {
+      const uint32_t np = std::min<uint32_t>(d->h_ctrl[frame], (uint32_t)g.cap_pts);
+      src = d->d.pts + (size_t)frame * g.cap_pts;
+      n = (size_t)np * 8;
+      break;
+    }
+    case AT_STAGE_BLOB_POINTS: {
+      // IndexPoint keys of the selected pairs, in rank order
+      const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[B + frame], (uint32_t)kMaxPairs);
+      std::vector<uint32_t> cnt(npairs), off(npairs), sel(npairs);
+      if (npairs) {
+        if (hipMemcpy(cnt.data(), d->d.pair_cnt + (size_t)frame * kMaxPairs, npairs * 4, hipMemcpyDeviceToHost) ||
+            hipMemcpy(off.data(), d->d.pair_off + (size_t)frame * kMaxPairs, npairs * 4, hipMemcpyDeviceToHost) ||
+            hipMemcpy(sel.data(), d->d.pair_sel + (size_t)frame * kMaxPairs, npairs * 4, hipMemcpyDeviceToHost))
+          return AT_E_HIP;
+      }
+      size_t total = 0;
+      for (uint32_t i = 0; i < npairs; i++)
+        if (sel[i]) total += cnt[i];
+      if (bytes < total * 8) return (long long)(total * 8);
+      size_t o = 0;
+      for (uint32_t i = 0; i < npairs; i++) {
+        if (!sel[i]) continue;
+        if (hipMemcpy((uint8_t*)dst + o * 8, d->d.grp + (size_t)frame * g.cap_pts + off[i], cnt[i] * 8,
+                      hipMemcpyDeviceToHost) != hipSuccess)
+          return AT_E_HIP;
+        o += cnt[i];
+      }
+      return (long long)(total * 8);
+    }
+    default: return AT_E_INVALID;
+  }
+  if (bytes < n) return AT_E_INVALID;
+  if (n && hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) != hipSuccess) return AT_E_HIP;
+  return (long long)n;
+}
+
+}  // extern "C"

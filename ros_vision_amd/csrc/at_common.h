@@ -1,0 +1,101 @@
+// at_common.h -- shared host/device definitions of the MI355X AprilTag stage.
+#pragma once
+
+#include <stdint.h>
+
+#include "at_detmath.h"
+
+namespace at {
+
+// ---- capacities -----------------------------------------------------------
+constexpr int kCclTile = 32;           // CCL tile edge in decimated pixels (16x16 2x2-blocks)
+constexpr int kHashSlots = 16384;      // per-frame open-addressing table of blob pairs
+constexpr int kHashBits = 14;
+constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
+constexpr int kMaxDets = 128;          // candidate detections per frame
+constexpr int kMaxQuads = 512;         // fitted-quad debug records per frame
+constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
+constexpr int kBlobThreads = 256;
+constexpr int kNMaxima = 10;
+
+// ---- per-frame status bits -------------------------------------------------
+constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs
+constexpr uint32_t kStatusHashFull = 2u;
+constexpr uint32_t kStatusDetsOverflow = 4u;
+constexpr uint32_t kStatusPointsOverflow = 8u;
+
+// Frame geometry (all derived from W, H).
+struct Geom {
+  int W, H, Wd, Hd;     // full / decimated
+  int TW, TH;           // 4x4 threshold tiles
+  int BW, BH;           // 2x2 CCL blocks
+  int CTX, CTY;         // CCL tiles
+  int cap_pts;          // 4 * (Wd-2) * (Hd-2)
+  uint32_t min_cluster; // max(24, min_cluster_pixels)
+  uint32_t max_cluster; // 2 * (W + H)
+  int min_tag_width;    // width_at_border / quad_decimate, >= 3
+};
+
+struct Params {
+  int min_white_black_diff;
+  float max_line_fit_mse;
+  double cos_critical_rad;
+  double decode_sharpening;
+  int refine_edges;
+  double fx, fy, cx, cy, k1, k2, p1, p2, k3;
+};
+
+// One detection candidate as produced on the device (before reconcile).
+struct DevDetection {
+  int32_t id, hamming;
+  float decision_margin;
+  int32_t blob_rank;
+  double H[9];
+  double c[2];
+  double p[4][2];
+};
+
+struct QuadRecord {
+  uint32_t blob_index, valid, accepted;
+  uint16_t indices[4];
+  float corners[4][2];
+};
+
+// Device buffers; every per-frame array is [max_batch][per-frame size].
+struct DevBufs {
+  const uint8_t* const* frames;   // device table of frame pointers
+  uint8_t* gray;      // [B][W*H]
+  uint8_t* dec;       // [B][Wd*Hd]
+  uint8_t* mm;        // [B][TW*TH*2]   unfiltered 4x4 min/max
+  uint8_t* thr;       // [B][Wd*Hd]
+  uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
+  uint32_t* lab;      // [B][Wd*Hd]
+  uint32_t* size;     // [B][Wd*Hd]
+  uint64_t* pts;      // [B][cap_pts]   boundary points, emission order
+  uint64_t* grp;      // [B][cap_pts]   boundary points grouped by pair rank
+  uint64_t* ht_key;   // [B][kHashSlots]
+  uint32_t* ht_cnt;   // [B][kHashSlots]
+  uint32_t* ht_rank;  // [B][kHashSlots]
+  uint32_t* ht_off;   // [B][kHashSlots]
+  uint32_t* ht_cur;   // [B][kHashSlots]
+  uint32_t* pair_cnt; // [B][kMaxPairs]
+  uint32_t* pair_off; // [B][kMaxPairs]
+  uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair
+  uint32_t* work;     // [B*kMaxPairs]   (frame << 16) | rank of candidate pairs
+  DevDetection* dets; // [B][kMaxDets]
+  QuadRecord* quads;  // [B][kMaxQuads]
+  // control block (zeroed every batch)
+  uint32_t* npts;     // [B]
+  uint32_t* npairs;   // [B]
+  uint32_t* ndets;    // [B]
+  uint32_t* nquads;   // [B]
+  uint32_t* status;   // [B]
+  uint32_t* nwork;    // [1]
+  uint32_t* workhead; // [1]
+  // per-workgroup scratch of the blob kernel
+  int32_t* s_i32;     // [nblobwg][3][kSortCap]  prefix Mx, My, W
+  int64_t* s_i64;     // [nblobwg][3][kSortCap]  prefix Mxx, Myy, Mxy
+  double* s_f64;      // [nblobwg][2][kSortCap]  errs, filtered errs
+};
+
+}  // namespace at

@@ -1,0 +1,1574 @@
+// at_kernels.hip -- gfx950 kernels of the AprilTag detection stage.
+//
+// Pipeline for a batch of B frames, all on one HIP stream, no host round trip
+// until the detections are copied back:
+//   k_pre          YUYV/BGR/GRAY -> gray, decimated, 4x4 tile min/max   (threshold.cu:16-80)
+//   k_thr_ccl      tile filter + threshold + LDS union-find per 32x32 tile (threshold.cu:84-147,
+//                  labeling_allegretti_2019_BKE.cu:114-338)
+//   k_ccl_border   unions across tile borders (global atomicMin)
+//   k_ccl_final    root labels + blob sizes                              (:340-462)
+//   k_boundary     boundary points + pair histogram, wave-compacted      (apriltag_gpu.cu:226-360,
+//                                                                         P1, P3 counts)
+//   k_pairs        rank pairs (rep1-major order), offsets, work list     (P2, P3, P4)
+//   k_group        scatter points into per-pair segments
+//   k_blob         per blob: extents, filter, theta sort, line fit, peaks, quad fit,
+//                  corners, refine edges, homography, decode             (P4-P10, K10, K11,
+//                                                                         apriltag_detect.cu)
+// All float arithmetic is compiled with -ffp-contract=off and uses at_detmath.h
+// for transcendental functions so that results are bit-identical to the CPU
+// oracle (oracle/ao_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "at_common.h"
+
+namespace at {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t mix_hash(uint64_t k) {
+  return (k * 0x9E3779B97F4A7C15ull) >> (64 - kHashBits);
+}
+
+// QuadBoundaryPoint direction decode (points.h:83-108): dxy 0:(1,0) 1:(1,1) 2:(0,1) 3:(-1,1)
+__device__ __forceinline__ int dx_of(int dxy) { return dxy == 3 ? -1 : (dxy == 2 ? 0 : 1); }
+__device__ __forceinline__ int dy_of(int dxy) { return dxy == 0 ? 0 : 1; }
+
+struct DevCodebook {
+  int n;
+  uint64_t code[96];
+  int id[96];
+};
+__constant__ DevCodebook c_book;
+
+// tag36h11 bit layout (apriltag 3.x)
+__constant__ int c_bitx[36] = {1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4,
+                               6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3};
+__constant__ int c_bity[36] = {1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3,
+                               6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4};
+__constant__ float c_filter[7] = {0.01110899634659290314f, 0.13533528149127960205f, 0.60653066635131835938f,
+                                  1.00000000000000000000f, 0.60653066635131835938f, 0.13533528149127960205f,
+                                  0.01110899634659290314f};
+
+// ---------------------------------------------------------------------------
+// K1: gray / decimate / 4x4 tile min-max.  One thread per 4x4 decimated tile
+// (8x8 full-resolution pixels).  YUYV rows are read as 16-byte loads, so a
+// wave reads 1 KiB contiguous per row.
+// ---------------------------------------------------------------------------
+template <int FMT>
+__global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
+  const int f = blockIdx.z;
+  const int tx = blockIdx.x * 64 + threadIdx.x;
+  const int ty = blockIdx.y * 4 + threadIdx.y;
+  if (tx >= g.TW || ty >= g.TH) return;
+  const uint8_t* in = b.frames[f];
+  uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
+  uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+  uint32_t mn = 255, mx = 0;
+  const int x0 = tx * 8;
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int row = ty * 8 + r;
+    uint32_t y[8];
+    if (FMT == 0) {  // YUYV: Y at even bytes
+      const uint4 v = *reinterpret_cast<const uint4*>(in + ((size_t)row * g.W + x0) * 2);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        y[2 * k] = w[k] & 0xff;
+        y[2 * k + 1] = (w[k] >> 16) & 0xff;
+      }
+    } else if (FMT == 1) {  // BGR8 -> Y (OpenCV BGR2YUV_YUYV, ITUR_BT_601_SHIFT 20)
+      const uint8_t* p = in + ((size_t)row * g.W + x0) * 3;
+      const uint2 v0 = *reinterpret_cast<const uint2*>(p);
+      const uint2 v1 = *reinterpret_cast<const uint2*>(p + 8);
+      const uint2 v2 = *reinterpret_cast<const uint2*>(p + 16);
+      uint8_t bytes[24];
+      *reinterpret_cast<uint2*>(bytes) = v0;
+      *reinterpret_cast<uint2*>(bytes + 8) = v1;
+      *reinterpret_cast<uint2*>(bytes + 16) = v2;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int bb = bytes[3 * k], gg = bytes[3 * k + 1], rr = bytes[3 * k + 2];
+        y[k] = (uint32_t)((269484 * rr + 528482 * gg + 102760 * bb + (1 << 19) + (16 << 20)) >> 20);
+      }
+    } else {  // GRAY8
+      const uint2 v = *reinterpret_cast<const uint2*>(in + (size_t)row * g.W + x0);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        y[k] = (v.x >> (8 * k)) & 0xff;
+        y[4 + k] = (v.y >> (8 * k)) & 0xff;
+      }
+    }
+    uint2 gw;
+    gw.x = y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24);
+    gw.y = y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24);
+    *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x0) = gw;
+    if ((r & 1) == 0) {
+      const uint32_t d = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
+      *reinterpret_cast<uint32_t*>(dec + (size_t)(row >> 1) * g.Wd + (x0 >> 1)) = d;
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        mn = min(mn, y[k]);
+        mx = max(mx, y[k]);
+      }
+    }
+  }
+  uint8_t* mm = b.mm + (size_t)f * g.TW * g.TH * 2;
+  *reinterpret_cast<uint16_t*>(mm + 2 * ((size_t)ty * g.TW + tx)) = (uint16_t)(mn | (mx << 8));
+}
+
+// ---------------------------------------------------------------------------
+// K3: threshold + tile-local union-find.
+// One 256-thread workgroup per 32x32 decimated tile; thread (ty,tx) owns
+// 2x2 block (ty,tx).  Node slots in LDS are ordered like the global node ids
+// (per block row: 16 foreground nodes, then 32 background L/R nodes), so
+// "link to the smaller slot" == "link to the smaller id" and every local root
+// is the minimum node id of its local component.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_find(volatile uint32_t* par, uint32_t n) {
+  uint32_t p = par[n];
+  while (p != n) {
+    n = p;
+    p = par[n];
+  }
+  return n;
+}
+
+__device__ void lds_union(uint32_t* par, uint32_t a, uint32_t b) {
+  volatile uint32_t* vp = par;
+  while (true) {
+    a = lds_find(vp, a);
+    b = lds_find(vp, b);
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t old = atomicMin(&par[b], a);
+      if (old == b) return;
+      b = old;
+    } else {
+      const uint32_t old = atomicMin(&par[a], b);
+      if (old == a) return;
+      a = old;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t slot_of(int ty, int tx, int type) {
+  return (uint32_t)(ty * 48 + (type == 0 ? tx : 16 + 2 * tx + (type - 1)));
+}
+
+__global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
+  const int f = blockIdx.z;
+  const int tid = threadIdx.x;
+  const int y0 = blockIdx.y * kCclTile, x0 = blockIdx.x * kCclTile;
+  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+  const uint8_t* mm = b.mm + (size_t)f * g.TW * g.TH * 2;
+  uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
+
+  __shared__ uint8_t s_umn[11][12], s_umx[11][12];
+  __shared__ uint8_t s_fmn[9][10], s_fmx[9][10];
+  __shared__ uint8_t s_t[33][36];  // thr of rows y0-1..y0+31, cols x0-1..x0+32 (+pad)
+  __shared__ uint32_t s_par[768];
+  __shared__ uint32_t s_cnt[768];
+
+  // zero this tile's share of the frame's pair hash table (used by k_boundary)
+  {
+    const int ntiles = g.CTX * g.CTY;
+    const int tile = blockIdx.y * g.CTX + blockIdx.x;
+    const int per = (kHashSlots + ntiles - 1) / ntiles;
+    const int s0 = tile * per;
+    for (int i = tid; i < per; i += 256) {
+      const int s = s0 + i;
+      if (s < kHashSlots) {
+        b.ht_key[(size_t)f * kHashSlots + s] = 0;
+        b.ht_cnt[(size_t)f * kHashSlots + s] = 0;
+      }
+    }
+  }
+
+  // unfiltered tile min/max for tile rows ty0-2..ty0+8, cols tx0-2..tx0+9
+  const int ty0 = y0 / 4, tx0 = x0 / 4;
+  for (int i = tid; i < 11 * 12; i += 256) {
+    const int r = i / 12, c = i % 12;
+    const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
+    uint8_t mn = 255, mx = 0;  // out of range: neutral for min/max
+    if (tr >= 0 && tr < g.TH && tc >= 0 && tc < g.TW) {
+      const uint16_t v = *reinterpret_cast<const uint16_t*>(mm + 2 * ((size_t)tr * g.TW + tc));
+      mn = v & 0xff;
+      mx = v >> 8;
+    }
+    s_umn[r][c] = mn;
+    s_umx[r][c] = mx;
+  }
+  __syncthreads();
+  // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+7
+  for (int i = tid; i < 9 * 10; i += 256) {
+    const int r = i / 10, c = i % 10;
+    uint8_t mn = 255, mx = 0;
+#pragma unroll
+    for (int dr = 0; dr < 3; dr++)
+#pragma unroll
+      for (int dc = 0; dc < 3; dc++) {
+        mn = min(mn, s_umn[r + dr][c + dc]);
+        mx = max(mx, s_umx[r + dr][c + dc]);
+      }
+    s_fmn[r][c] = mn;
+    s_fmx[r][c] = mx;
+  }
+  __syncthreads();
+  // InternalThreshold for the 33x34 halo region; outside the image -> 127
+  for (int i = tid; i < 33 * 34; i += 256) {
+    const int r = i / 34, c = i % 34;
+    const int y = y0 - 1 + r, x = x0 - 1 + c;
+    uint8_t res = 127;
+    if (y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) {
+      const int fr = (y >> 2) - (ty0 - 1), fc = (x >> 2) - (tx0 - 1);
+      const int mn = s_fmn[fr][fc], mx = s_fmx[fr][fc];
+      if (mx - mn < prm.min_white_black_diff) {
+        res = 127;
+      } else {
+        const uint8_t th = (uint8_t)(mn + (mx - mn) / 2);
+        res = dec[(size_t)y * g.Wd + x] > th ? 255 : 0;
+      }
+    }
+    s_t[r][c] = res;
+  }
+  for (int i = tid; i < 768; i += 256) {
+    s_par[i] = i;
+    s_cnt[i] = 0;
+  }
+  __syncthreads();
+  // write this tile's threshold plane (4 bytes per thread)
+  {
+    const int r = tid >> 3, c4 = (tid & 7) * 4;
+    const int y = y0 + r, x = x0 + c4;
+    if (y < g.Hd && x < g.Wd) {
+      const uint32_t w = s_t[r + 1][c4 + 1] | (s_t[r + 1][c4 + 2] << 8) | (s_t[r + 1][c4 + 3] << 16) |
+                         ((uint32_t)s_t[r + 1][c4 + 4] << 24);
+      *reinterpret_cast<uint32_t*>(thr + (size_t)y * g.Wd + x) = w;
+    }
+  }
+  // local unions over intra-tile edges (InitLabeling P/Q/R/S + Merge)
+  const int bty = tid >> 4, btx = tid & 15;
+#define T(rr, cc) s_t[(rr) + 1][(cc) + 1]
+  const int pr = 2 * bty, pc = 2 * btx;
+  const uint8_t a = T(pr, pc), bb = T(pr, pc + 1), c = T(pr + 1, pc), d = T(pr + 1, pc + 1);
+  const uint32_t F = slot_of(bty, btx, 0), L = slot_of(bty, btx, 1), R = slot_of(bty, btx, 2);
+  if (bty > 0) {
+    if (btx > 0 && a == 255 && T(pr - 1, pc - 1) == 255) lds_union(s_par, F, slot_of(bty - 1, btx - 1, 0));
+    if ((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255))
+      lds_union(s_par, F, slot_of(bty - 1, btx, 0));
+    if (btx < 15 && bb == 255 && T(pr - 1, pc + 2) == 255) lds_union(s_par, F, slot_of(bty - 1, btx + 1, 0));
+    if (a == 0 && T(pr - 1, pc) == 0) lds_union(s_par, L, slot_of(bty - 1, btx, 1));
+    if (bb == 0 && T(pr - 1, pc + 1) == 0) lds_union(s_par, R, slot_of(bty - 1, btx, 2));
+  }
+  if (btx > 0) {
+    if ((a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255))
+      lds_union(s_par, F, slot_of(bty, btx - 1, 0));
+    if ((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0))
+      lds_union(s_par, L, slot_of(bty, btx - 1, 2));
+  }
+  if ((a == 0 && bb == 0) || (c == 0 && d == 0)) lds_union(s_par, R, L);
+#undef T
+  __syncthreads();
+  const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
+  __syncthreads();
+  s_par[F] = rF;
+  s_par[L] = rL;
+  s_par[R] = rR;
+  const uint32_t nfg = (a == 255) + (bb == 255) + (c == 255) + (d == 255);
+  const uint32_t nbl = (a == 0) + (c == 0), nbr = (bb == 0) + (d == 0);
+  if (nfg) atomicAdd(&s_cnt[rF], nfg);
+  if (nbl) atomicAdd(&s_cnt[rL], nbl);
+  if (nbr) atomicAdd(&s_cnt[rR], nbr);
+  __syncthreads();
+  // publish: gpar[node] = global id of its local root; size[root] = local pixel count
+  const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
+  if (BY < g.BH && BX < g.BW) {
+    auto gid = [&](uint32_t s) -> uint32_t {
+      const int sty = s / 48, r = s % 48;
+      const int gy = y0 / 2 + sty;
+      if (r < 16) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
+      const int k = r - 16;
+      return (uint32_t)((2 * gy + 1) * g.Wd + 2 * (x0 / 2 + (k >> 1)) + (k & 1));
+    };
+    uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
+    uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
+    const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
+    const uint32_t idL = idF + g.Wd;
+    *reinterpret_cast<uint2*>(par + idF) = make_uint2(gid(rF), idF + 1);
+    *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL), gid(rR));
+    *reinterpret_cast<uint2*>(size + idF) = make_uint2(rF == F ? s_cnt[F] : 0u, 0u);
+    *reinterpret_cast<uint2*>(size + idL) = make_uint2(rL == L ? s_cnt[L] : 0u, rR == R ? s_cnt[R] : 0u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4: unions across CCL tile borders.  One wave per tile: lanes 0-15 own the
+// tile's top block row (P, Q, R, bg Q), lanes 16-31 its left block column
+// (S, bg S, P for rows >= 1), lanes 32-46 its right column (R for rows >= 1).
+// Global union-find with atomicMin links to the smaller id; stale reads are
+// tolerated because every link is decided by the atomic's return value.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t g_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ uint32_t g_find(uint32_t* par, uint32_t n) {
+  uint32_t p = g_load(par + n);
+  while (p != n) {
+    n = p;
+    p = g_load(par + n);
+  }
+  return n;
+}
+__device__ void g_union(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    a = g_find(par, a);
+    b = g_find(par, b);
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t old = atomicMin(par + b, a);
+      if (old == b) return;
+      b = old;
+    } else {
+      const uint32_t old = atomicMin(par + a, b);
+      if (old == a) return;
+      a = old;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
+  const int f = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int tile_x = blockIdx.x, tile_y = blockIdx.y;
+  int bty, btx, role;
+  if (lane < 16) { role = 0; bty = 0; btx = lane; }
+  else if (lane < 32) { role = 1; bty = lane - 16; btx = 0; }
+  else if (lane < 47) { role = 2; bty = lane - 31; btx = 15; }
+  else return;
+  const int BY = tile_y * 16 + bty, BX = tile_x * 16 + btx;
+  if (BY >= g.BH || BX >= g.BW) return;
+  const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
+  uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
+  const int Wd = g.Wd;
+  const int row = 2 * BY, col = 2 * BX;
+  const size_t idx = (size_t)row * Wd + col;
+  auto px = [&](int r, int c) -> uint8_t {
+    if (r < 0 || c < 0 || r >= g.Hd || c >= g.Wd) return 127;
+    return thr[(size_t)r * Wd + c];
+  };
+  const uint8_t a = thr[idx], bb = thr[idx + 1], c = thr[idx + Wd];
+  const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
+  if (role == 0 && BY > 0) {
+    if (a == 255 && px(row - 1, col - 1) == 255) g_union(par, F, F - 2 * Wd - 2);
+    if ((a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255))
+      g_union(par, F, F - 2 * Wd);
+    if (bb == 255 && px(row - 1, col + 2) == 255) g_union(par, F, F - 2 * Wd + 2);
+    if (a == 0 && px(row - 1, col) == 0) g_union(par, L, L - 2 * Wd);
+    if (bb == 0 && px(row - 1, col + 1) == 0) g_union(par, R, R - 2 * Wd);
+  }
+  if (role == 1 && BX > 0) {
+    if (BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255) g_union(par, F, F - 2 * Wd - 2);
+    if ((a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255)) g_union(par, F, F - 2);
+    if ((a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0)) g_union(par, L, L - 1);
+  }
+  if (role == 2 && BY > 0) {
+    if (bb == 255 && px(row - 1, col + 2) == 255) g_union(par, F, F - 2 * Wd + 2);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5: final labels (FinalLabeling, :340-462) and blob sizes.  One thread per
+// 2x2 block.  Local-root pixel counts move to the global root with one atomic
+// per local component instead of one per block.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t plain_find(const uint32_t* par, uint32_t n) {
+  uint32_t p = par[n];
+  while (p != n) {
+    n = p;
+    p = par[n];
+  }
+  return n;
+}
+
+__global__ __launch_bounds__(256) void k_ccl_final(DevBufs b, Geom g) {
+  const int f = blockIdx.z;
+  const int BX = blockIdx.x * 64 + threadIdx.x;
+  const int BY = blockIdx.y * 4 + threadIdx.y;
+  if (BX >= g.BW || BY >= g.BH) return;
+  const size_t fo = (size_t)f * g.Wd * g.Hd;
+  const uint8_t* thr = b.thr + fo;
+  const uint32_t* par = b.par + fo;
+  uint32_t* lab = b.lab + fo;
+  uint32_t* size = b.size + fo;
+  const int Wd = g.Wd;
+  const uint32_t idF = (uint32_t)(2 * BY * Wd + 2 * BX), idL = idF + Wd, idR = idL + 1;
+  const uint16_t top = *reinterpret_cast<const uint16_t*>(thr + idF);
+  const uint16_t bot = *reinterpret_cast<const uint16_t*>(thr + idL);
+  const uint8_t px[4] = {(uint8_t)(top & 0xff), (uint8_t)(top >> 8), (uint8_t)(bot & 0xff), (uint8_t)(bot >> 8)};
+  const bool any = px[0] != 127 || px[1] != 127 || px[2] != 127 || px[3] != 127;
+  if (!any) {
+    *reinterpret_cast<uint2*>(lab + idF) = make_uint2(idF, idF + 1);
+    *reinterpret_cast<uint2*>(lab + idL) = make_uint2(idL, idR);
+    return;
+  }
+  const uint32_t rF = plain_find(par, idF), rL = plain_find(par, idL), rR = plain_find(par, idR);
+  uint32_t l4[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    l4[k] = 0;
+    if (px[k] == 255) l4[k] = rF;
+    else if (px[k] == 0) l4[k] = (k == 0 || k == 2) ? rL : rR;
+  }
+  *reinterpret_cast<uint2*>(lab + idF) = make_uint2(l4[0], l4[1]);
+  *reinterpret_cast<uint2*>(lab + idL) = make_uint2(l4[2], l4[3]);
+  const uint32_t ids[3] = {idF, idL, idR}, roots[3] = {rF, rL, rR};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (roots[k] != ids[k]) {
+      const uint32_t cnt = size[ids[k]];
+      if (cnt) {
+        atomicAdd(size + roots[k], cnt);
+        size[ids[k]] = 0;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K6: boundary points (BlobDiff) fused with stream compaction and the pair
+// histogram.  Points are appended with one atomic per wave per direction; the
+// pair histogram is pre-aggregated over runs of equal pairs in consecutive
+// lanes (neighbouring pixels mostly border the same two blobs).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t make_qbp(uint32_t rep0, uint32_t rep1, uint32_t x, uint32_t y, int dxy,
+                                             bool b2w) {
+  const uint32_t lo = rep0 < rep1 ? rep0 : rep1, hi = rep0 < rep1 ? rep1 : rep0;
+  return ((uint64_t)(hi & 0xfffff) << 44) | ((uint64_t)(lo & 0xfffff) << 24) | ((uint64_t)(x & 0x3ff) << 14) |
+         ((uint64_t)(y & 0x3ff) << 4) | ((uint64_t)(b2w ? 1 : 0) << 3) | (uint64_t)(dxy & 3);
+}
+
+__device__ uint32_t ht_slot_insert(uint64_t* keys, uint64_t key) {
+  uint32_t s = (uint32_t)mix_hash(key);
+  for (int probe = 0; probe < kHashSlots; probe++) {
+    const uint64_t k = keys[s];
+    if (k == key) return s;
+    if (k == 0) {
+      const uint64_t prev = atomicCAS((unsigned long long*)(keys + s), 0ull, (unsigned long long)key);
+      if (prev == 0 || prev == key) return s;
+    }
+    s = (s + 1) & (kHashSlots - 1);
+  }
+  return 0xffffffffu;
+}
+
+__device__ uint32_t ht_slot_find(const uint64_t* keys, uint64_t key) {
+  uint32_t s = (uint32_t)mix_hash(key);
+  for (int probe = 0; probe < kHashSlots; probe++) {
+    const uint64_t k = keys[s];
+    if (k == key) return s;
+    if (k == 0) return 0xffffffffu;
+    s = (s + 1) & (kHashSlots - 1);
+  }
+  return 0xffffffffu;
+}
+
+// Length of the run of equal keys starting at this lane (only meaningful for
+// run heads); same_mask bit l means "lane l continues the run of lane l-1".
+__device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
+  if (lane == 63) return 1;
+  const uint64_t rest = ~(same_mask >> (lane + 1));
+  return 1 + (uint32_t)__builtin_ctzll(rest);
+}
+
+__global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
+  const int f = blockIdx.z;
+  const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+  const int y = 1 + blockIdx.y * 4 + threadIdx.y;
+  const size_t fo = (size_t)f * g.Wd * g.Hd;
+  const uint8_t* thr = b.thr + fo;
+  const uint32_t* lab = b.lab + fo;
+  const uint32_t* size = b.size + fo;
+  const int Wd = g.Wd;
+  uint64_t pk[4] = {0, 0, 0, 0};
+  if (x <= g.Wd - 2 && y <= g.Hd - 2) {
+    const size_t i0 = (size_t)y * Wd + x;
+    const uint8_t v0 = thr[i0];
+    const uint32_t rep0 = lab[i0];
+    if (v0 != 127 && size[rep0] >= 25) {
+      const uint8_t vr = thr[i0 + 1], vd = thr[i0 + Wd], vdr = thr[i0 + Wd + 1], vdl = thr[i0 + Wd - 1],
+                    vl = thr[i0 - 1];
+      const uint32_t lr = lab[i0 + 1], ld = lab[i0 + Wd], ldr = lab[i0 + Wd + 1], ldl = lab[i0 + Wd - 1],
+                     ll = lab[i0 - 1];
+      if (v0 + vr == 255 && size[lr] >= 25) pk[0] = make_qbp(rep0, lr, x, y, 0, vr > v0);
+      if (v0 + vdr == 255 && size[ldr] >= 25) pk[1] = make_qbp(rep0, ldr, x, y, 1, vdr > v0);
+      if (v0 + vd == 255 && size[ld] >= 25) pk[2] = make_qbp(rep0, ld, x, y, 2, vd > v0);
+      bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && size[ll] >= 25 && size[ld] >= 25;
+      if (!dedup && v0 + vdl == 255 && size[ldl] >= 25) pk[3] = make_qbp(rep0, ldl, x, y, 3, vdl > v0);
+    }
+  }
+  const uint32_t lane = lane_id();
+  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
+  uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
+  uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
+#pragma unroll
+  for (int dir = 0; dir < 4; dir++) {
+    const bool has = pk[dir] != 0;
+    const uint64_t m = __ballot(has);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(b.npts + f, (uint32_t)__popcll(m));
+    base = __shfl(base, 0);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (has) {
+      if (pos < (uint32_t)g.cap_pts) pts[pos] = pk[dir];
+      else atomicOr(b.status + f, kStatusPointsOverflow);
+    }
+    // pair histogram, aggregated over runs of equal pairs
+    const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
+    const uint64_t prev = __shfl_up(r01, 1);
+    const bool same = has && lane > 0 && prev == r01;
+    const uint64_t same_mask = __ballot(same);
+    if (has && !same) {
+      const uint32_t len = run_len(same_mask, lane);
+      const uint32_t s = ht_slot_insert(ht_key, r01);
+      if (s == 0xffffffffu) atomicOr(b.status + f, kStatusHashFull);
+      else atomicAdd(ht_cnt + s, len);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K7: rank the pairs of a frame (P2 radix order: rep1 major, rep0 minor ==
+// numeric order of rep01), assign each its segment offset, and append the
+// pairs whose point count passes the size filter to the global work list.
+// One 1024-thread workgroup per frame; bitonic sort in LDS.
+// ---------------------------------------------------------------------------
+template <typename T, int NT>
+__device__ void block_bitonic_sort(T* s, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const T a = s[i], c = s[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) {
+            s[i] = c;
+            s[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ uint64_t s_list[kMaxPairs];
+  __shared__ uint32_t s_cnt[kMaxPairs];
+  __shared__ uint32_t s_n;
+  __shared__ uint32_t s_wsum[16];
+  const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
+  const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  for (int s = tid; s < kHashSlots; s += 1024) {
+    const uint64_t k = ht_key[s];
+    if (k) {
+      const uint32_t i = atomicAdd(&s_n, 1u);
+      if (i < kMaxPairs) s_list[i] = (k << kHashBits) | (uint64_t)s;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = s_n;
+  if (tid == 0) b.npairs[f] = n;
+  if (n > (uint32_t)kMaxPairs) {
+    if (tid == 0) atomicOr(b.status + f, kStatusPairsOverflow);
+    return;
+  }
+  int np2 = 64;
+  while (np2 < (int)n) np2 <<= 1;
+  for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
+  __syncthreads();
+  block_bitonic_sort<uint64_t, 1024>(s_list, np2);
+  // counts in rank order, exclusive scan -> offsets
+  for (int i = tid; i < kMaxPairs; i += 1024)
+    s_cnt[i] = i < (int)n ? ht_cnt[s_list[i] & (kHashSlots - 1)] : 0u;
+  __syncthreads();
+  // each thread owns 4 consecutive ranks
+  const int i0 = tid * 4;
+  const uint32_t c0 = s_cnt[i0], c1 = s_cnt[i0 + 1], c2 = s_cnt[i0 + 2], c3 = s_cnt[i0 + 3];
+  const uint32_t tsum = c0 + c1 + c2 + c3;
+  uint32_t incl = tsum;
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  if (lane == 63) s_wsum[tid >> 6] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int w = 0; w < (tid >> 6); w++) wbase += s_wsum[w];
+  const uint32_t excl = wbase + incl - tsum;
+  const uint32_t offs[4] = {excl, excl + c0, excl + c0 + c1, excl + c0 + c1 + c2};
+  const uint32_t cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + k;
+    if (i < (int)n) {
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      b.ht_rank[(size_t)f * kHashSlots + slot] = (uint32_t)i;
+      b.ht_off[(size_t)f * kHashSlots + slot] = offs[k];
+      b.ht_cur[(size_t)f * kHashSlots + slot] = 0;
+      b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
+      b.pair_off[(size_t)f * kMaxPairs + i] = offs[k];
+      b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
+      if (cs[k] >= g.min_cluster && cs[k] <= g.max_cluster) {
+        const uint32_t w = atomicAdd(b.nwork, 1u);
+        b.work[w] = ((uint32_t)f << 16) | (uint32_t)i;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K8: scatter the points into their pair segments (grouped by pair rank).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
+  const int f = blockIdx.y;
+  if (b.status[f] & (kStatusPairsOverflow | kStatusHashFull)) return;
+  const uint32_t n = b.npts[f];
+  const uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
+  uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
+  const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
+  const uint32_t* ht_off = b.ht_off + (size_t)f * kHashSlots;
+  uint32_t* ht_cur = b.ht_cur + (size_t)f * kHashSlots;
+  const uint32_t lane = lane_id();
+  const uint32_t stride = gridDim.x * 256;
+  const uint32_t nround = (n + stride - 1) / stride;
+  for (uint32_t r = 0; r < nround; r++) {
+    const uint32_t i = r * stride + blockIdx.x * 256 + threadIdx.x;
+    const bool has = i < n;
+    const uint64_t key = has ? pts[i] : 0;
+    const uint64_t r01 = key >> 24;
+    const uint32_t slot = has ? ht_slot_find(ht_key, r01) : 0xffffffffu;
+    const uint32_t prev = __shfl_up(slot, 1);
+    const bool same = has && lane > 0 && prev == slot;
+    const uint64_t same_mask = __ballot(same);
+    const uint64_t head_mask = __ballot(has && !same);
+    uint32_t base = 0;
+    if (has && !same) base = atomicAdd(ht_cur + slot, run_len(same_mask, lane));
+    const uint64_t upto = head_mask & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+    const uint32_t head = upto ? 63 - __clzll(upto) : 0;
+    const uint32_t hb = __shfl(base, head);
+    if (has) grp[ht_off[slot] + hb + (lane - head)] = key;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K9: one blob pair per workgroup iteration (persistent, work-list driven).
+// ---------------------------------------------------------------------------
+struct Ext {
+  uint32_t min_x, min_y, max_x, max_y, count;
+  int32_t gx_sum, gy_sum;
+  int64_t pg_sum;
+};
+
+__device__ __forceinline__ double ext_cx(const Ext& e) { return (double)((float)(e.min_x + e.max_x) * 0.5f) + 0.05118; }
+__device__ __forceinline__ double ext_cy(const Ext& e) {
+  return (double)((float)(e.min_y + e.max_y) * 0.5f) + -0.028581;
+}
+__device__ __forceinline__ float ext_dot(const Ext& e) {
+  const int64_t t = e.pg_sum * 2 - (int64_t)((int)(e.min_x + e.max_x) * e.gx_sum) -
+                    (int64_t)((int)(e.min_y + e.max_y) * e.gy_sum);
+  const double a = (double)t * 0.5;
+  const double bq = 0.05118 * (double)e.gx_sum;
+  const double c = 0.028581 * (double)e.gy_sum;
+  return (float)(a - bq + c);
+}
+
+struct Moments {
+  int32_t Mx, My, W;
+  int64_t Mxx, Myy, Mxy;
+  int32_t N;
+};
+
+struct BlobScratch {
+  int32_t *Mx, *My, *W;
+  int64_t *Mxx, *Myy, *Mxy;
+  double *err, *filt;
+};
+
+__device__ __forceinline__ Moments read_moments(const BlobScratch& P, uint32_t n, uint32_t i0, uint32_t i1) {
+  Moments m;
+  if (i0 < i1) {
+    m.N = (int32_t)(i1 - i0 + 1);
+    m.Mx = P.Mx[i1]; m.My = P.My[i1]; m.W = P.W[i1];
+    m.Mxx = P.Mxx[i1]; m.Myy = P.Myy[i1]; m.Mxy = P.Mxy[i1];
+    if (i0 > 0) {
+      m.Mx = (int32_t)((uint32_t)m.Mx - (uint32_t)P.Mx[i0 - 1]);
+      m.My = (int32_t)((uint32_t)m.My - (uint32_t)P.My[i0 - 1]);
+      m.W = (int32_t)((uint32_t)m.W - (uint32_t)P.W[i0 - 1]);
+      m.Mxx -= P.Mxx[i0 - 1]; m.Myy -= P.Myy[i0 - 1]; m.Mxy -= P.Mxy[i0 - 1];
+    }
+  } else {
+    const uint32_t a = i0 - 1, z = n - 1;
+    m.Mx = (int32_t)((uint32_t)P.Mx[z] - (uint32_t)P.Mx[a] + (uint32_t)P.Mx[i1]);
+    m.My = (int32_t)((uint32_t)P.My[z] - (uint32_t)P.My[a] + (uint32_t)P.My[i1]);
+    m.W = (int32_t)((uint32_t)P.W[z] - (uint32_t)P.W[a] + (uint32_t)P.W[i1]);
+    m.Mxx = P.Mxx[z] - P.Mxx[a] + P.Mxx[i1];
+    m.Myy = P.Myy[z] - P.Myy[a] + P.Myy[i1];
+    m.Mxy = P.Mxy[z] - P.Mxy[a] + P.Mxy[i1];
+    m.N = (int32_t)(n - i0 + i1 + 1);
+  }
+  return m;
+}
+
+// FitLine (line_fit_filter.cu:798-872) / HostFitLine (apriltag_detect.cu:38-90)
+__device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* err, double* mse) {
+  const int64_t W = m.W;
+  const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)W - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
+  const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)W - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
+  const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)W - (uint64_t)((int64_t)m.My * (int64_t)m.My));
+  const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
+  const float e8 = (float)((double)(W * W) * 8.0);
+  const float eig = ((float)(Cxx + Cyy) - h) / e8;
+  if (lp01) {
+    lp01[0] = (double)((float)m.Mx / (float)(m.W * 2));
+    lp01[1] = (double)((float)m.My / (float)(m.W * 2));
+  }
+  if (lp23) {
+    const float nx1 = (float)(Cxx - Cyy) - h, ny1 = (float)(2 * Cxy);
+    const float M1 = nx1 * nx1 + ny1 * ny1;
+    const float nx2 = (float)(2 * Cxy), ny2 = (float)(Cyy - Cxx) - h;
+    const float M2 = nx2 * nx2 + ny2 * ny2;
+    float nx, ny;
+    if (M1 > M2) { nx = nx1; ny = ny1; } else { nx = nx2; ny = ny2; }
+    const float len = det_hypotf(nx, ny);
+    lp23[0] = (double)(nx / len);
+    lp23[1] = (double)(ny / len);
+  }
+  *err = (double)((float)m.N * eig);
+  *mse = (double)eig;
+}
+
+// ---- block reductions (256 threads = 4 waves) ------------------------------
+template <typename T, typename Op>
+__device__ T wave_reduce(T v, Op op) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = op(v, __shfl_xor(v, d));
+  return v;
+}
+
+struct MinOp { template <typename T> __device__ T operator()(T a, T c) const { return a < c ? a : c; } };
+struct MaxOp { template <typename T> __device__ T operator()(T a, T c) const { return a > c ? a : c; } };
+struct AddOp { template <typename T> __device__ T operator()(T a, T c) const { return a + c; } };
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, Op op, T* s_tmp /* >= 4 */) {
+  v = wave_reduce(v, op);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) s_tmp[w] = v;
+  __syncthreads();
+  T r = s_tmp[0];
+  for (int i = 1; i < kBlobThreads / 64; i++) r = op(r, s_tmp[i]);
+  return r;
+}
+
+// inclusive block scan of one value per thread (256 threads); returns the
+// inclusive prefix, *total = block sum
+template <typename T>
+__device__ T block_incl_scan(T v, T* s_tmp, T* total) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T u = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v = v + u;
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 63) s_tmp[w] = v;
+  __syncthreads();
+  T base = 0;
+  for (int i = 0; i < w; i++) base = base + s_tmp[i];
+  *total = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+  return base + v;
+}
+
+
+__device__ void redistort(const Params& p, double* x, double* y) {
+  const double xP = (*x - p.cx) / p.fx, yP = (*y - p.cy) / p.fy;
+  const double rSq = xP * xP + yP * yP;
+  const double lin = 1 + p.k1 * rSq + p.k2 * rSq * rSq + p.k3 * rSq * rSq * rSq;
+  const double xPP = xP * lin + 2 * p.p1 * xP * yP + p.p2 * (rSq + 2 * xP * xP);
+  const double yPP = yP * lin + p.p1 * (rSq + 2 * yP * yP) + 2 * p.p2 * xP * yP;
+  *x = xPP * p.fx + p.cx;
+  *y = yPP * p.fy + p.cy;
+}
+
+__device__ void undistort(const Params& p, double* u, double* v) {
+  const double xPP = (*u - p.cx) / p.fx, yPP = (*v - p.cy) / p.fy;
+  double xP = xPP, yP = yPP;
+  const double x0 = xP, y0 = yP;
+  double prev_x, prev_y;
+  int it = 0;
+  do {
+    prev_x = xP;
+    prev_y = yP;
+    const double rSq = xP * xP + yP * yP;
+    const double rad = 1 + (p.k1 * rSq) + (p.k2 * rSq * rSq) + (p.k3 * rSq * rSq * rSq);
+    const double rinv = 1 / rad;
+    const double tdx = 2 * p.p1 * xP * yP + p.p2 * (rSq + p.k3 * rSq * rSq * rSq);  // apriltag_detect.cu:372
+    const double tdy = p.p1 * (rSq + 2 * yP * yP) + 2 * p.p2 * xP * yP;
+    xP = (x0 - tdx) * rinv;
+    yP = (y0 - tdy) * rinv;
+    if (it > 100) break;
+    it++;
+  } while (fabs(xP - prev_x) > 1e-6 || fabs(yP - prev_y) > 1e-6);
+  *u = xP * p.fx + p.cx;
+  *v = yP * p.fy + p.cy;
+}
+
+__device__ void hproject(const double* H, double x, double y, double* ox, double* oy) {
+  const double xx = H[0] * x + H[1] * y + H[2];
+  const double yy = H[3] * x + H[4] * y + H[5];
+  const double zz = H[6] * x + H[7] * y + H[8];
+  *ox = xx / zz;
+  *oy = yy / zz;
+}
+
+__device__ int homography_compute2(const double c[4][4], double* H) {
+  double A[72];
+  for (int i = 0; i < 4; i++) {
+    double* r0 = &A[(2 * i) * 9];
+    double* r1 = &A[(2 * i + 1) * 9];
+    r0[0] = c[i][0]; r0[1] = c[i][1]; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0;
+    r0[6] = -c[i][0] * c[i][2]; r0[7] = -c[i][1] * c[i][2]; r0[8] = c[i][2];
+    r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = c[i][0]; r1[4] = c[i][1]; r1[5] = 1;
+    r1[6] = -c[i][0] * c[i][3]; r1[7] = -c[i][1] * c[i][3]; r1[8] = c[i][3];
+  }
+  for (int col = 0; col < 8; col++) {
+    double max_val = 0;
+    int max_idx = -1;
+    for (int row = col; row < 8; row++) {
+      const double v = fabs(A[row * 9 + col]);
+      if (v > max_val) { max_val = v; max_idx = row; }
+    }
+    if (max_val < 1e-10) return -1;
+    if (max_idx != col)
+      for (int i = col; i < 9; i++) {
+        const double t = A[col * 9 + i];
+        A[col * 9 + i] = A[max_idx * 9 + i];
+        A[max_idx * 9 + i] = t;
+      }
+    for (int i = col + 1; i < 8; i++) {
+      const double fct = A[i * 9 + col] / A[col * 9 + col];
+      A[i * 9 + col] = 0;
+      for (int j = col + 1; j < 9; j++) A[i * 9 + j] -= fct * A[col * 9 + j];
+    }
+  }
+  for (int col = 7; col >= 0; col--) {
+    double sum = 0;
+    for (int i = col + 1; i < 8; i++) sum += A[col * 9 + i] * A[i * 9 + 8];
+    A[col * 9 + 8] = (A[col * 9 + 8] - sum) / A[col * 9 + col];
+  }
+  H[0] = A[8]; H[1] = A[17]; H[2] = A[26]; H[3] = A[35]; H[4] = A[44]; H[5] = A[53];
+  H[6] = A[62]; H[7] = A[71]; H[8] = 1;
+  return 0;
+}
+
+struct GrayModel {
+  double A[3][3], B[3], C[3];
+};
+__device__ void gm_add(GrayModel& g, double x, double y, double gray) {
+  g.A[0][0] += x * x; g.A[0][1] += x * y; g.A[0][2] += x;
+  g.A[1][1] += y * y; g.A[1][2] += y; g.A[2][2] += 1;
+  g.B[0] += x * gray; g.B[1] += y * gray; g.B[2] += gray;
+}
+__device__ void gm_solve(GrayModel& g) {
+  const double* A = &g.A[0][0];
+  double L[9], M[9];
+  L[0] = sqrt(A[0]); L[3] = A[1] / L[0]; L[6] = A[2] / L[0];
+  L[4] = sqrt(A[4] - L[3] * L[3]); L[7] = (A[5] - L[3] * L[6]) / L[4];
+  L[8] = sqrt(A[8] - L[6] * L[6] - L[7] * L[7]);
+  M[0] = 1 / L[0]; M[3] = -L[3] * M[0] / L[4]; M[4] = 1 / L[4];
+  M[6] = (-L[6] * M[0] - L[7] * M[3]) / L[8]; M[7] = -L[7] * M[4] / L[8]; M[8] = 1 / L[8];
+  const double t0 = M[0] * g.B[0];
+  const double t1 = M[3] * g.B[0] + M[4] * g.B[1];
+  const double t2 = M[6] * g.B[0] + M[7] * g.B[1] + M[8] * g.B[2];
+  g.C[0] = M[0] * t0 + M[3] * t1 + M[6] * t2;
+  g.C[1] = M[4] * t1 + M[7] * t2;
+  g.C[2] = M[8] * t2;
+}
+__device__ __forceinline__ double gm_interp(const GrayModel& g, double x, double y) {
+  return g.C[0] * x + g.C[1] * y + g.C[2];
+}
+
+__device__ __forceinline__ uint64_t rotate90_36(uint64_t w) {
+  return ((w << 9) | (w >> 27)) & ((1ull << 36) - 1);
+}
+
+__device__ __forceinline__ void unrank(int t, int* m) {
+  int c = 0;
+  for (int a = 0; a < 10; a++)
+    for (int bq = a + 1; bq < 10; bq++)
+      for (int d = bq + 1; d < 10; d++)
+        for (int e = d + 1; e < 10; e++) {
+          if (c == t) { m[0] = a; m[1] = bq; m[2] = d; m[3] = e; return; }
+          c++;
+        }
+}
+
+struct BlobShared {
+  union {
+    uint64_t keys[kSortCap];                 // point sort keys, later peak keys
+    struct { double sx[kSortCap / 2]; double sy[kSortCap / 2]; } smp;  // refine samples
+  } u;
+  double red_f64[4];
+  int64_t red_i64[4];
+  uint32_t red_u32[4];
+  int32_t red_i32[4];
+  uint64_t red_u64[4];
+  uint32_t item, nwork, npeaks, best_code;
+  int32_t pi[16];
+  double e01[7][7];
+  double lp01[7][7][2];
+  double combo_err[210];
+  int ok;
+  float qc[4][2];
+  int nsamp[4], samp_off[4];
+  float enx[4], eny[4];
+  double lines[4][4];
+  double H[9];
+  double gmx[64], gmy[64], gmv[64];
+  int gmvalid[64];
+  double values[100];
+};
+
+__global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params prm) {
+  __shared__ BlobShared S;
+  const int tid = threadIdx.x;
+  BlobScratch P;
+  {
+    const size_t wg = blockIdx.x;
+    P.Mx = b.s_i32 + (wg * 3 + 0) * kSortCap;
+    P.My = b.s_i32 + (wg * 3 + 1) * kSortCap;
+    P.W = b.s_i32 + (wg * 3 + 2) * kSortCap;
+    P.Mxx = b.s_i64 + (wg * 3 + 0) * kSortCap;
+    P.Myy = b.s_i64 + (wg * 3 + 1) * kSortCap;
+    P.Mxy = b.s_i64 + (wg * 3 + 2) * kSortCap;
+    P.err = b.s_f64 + (wg * 2 + 0) * kSortCap;
+    P.filt = b.s_f64 + (wg * 2 + 1) * kSortCap;
+  }
+  if (tid == 0) S.nwork = *b.nwork;
+  __syncthreads();
+  const uint32_t nwork = S.nwork;
+  while (true) {
+    if (tid == 0) S.item = atomicAdd(b.workhead, 1u);
+    __syncthreads();
+    const uint32_t item = S.item;
+    __syncthreads();
+    if (item >= nwork) break;
+    const uint32_t w = b.work[item];
+    const int f = (int)(w >> 16);
+    const uint32_t rank = w & 0xffff;
+    const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+    const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
+    uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
+    const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+    const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
+
+    // ---- extents (P3) ---------------------------------------------------------
+    uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
+    int32_t sgx = 0, sgy = 0;
+    int64_t spg = 0;
+    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+      const uint64_t k = grp[t];
+      S.u.keys[t] = k;
+      const int dxy = (int)(k & 3);
+      const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
+      const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
+      const bool b2w = (k & 8) != 0;
+      const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
+      mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
+      sgx += gx; sgy += gy;
+      spg += (int64_t)px * gx + (int64_t)py * gy;
+    }
+    Ext e;
+    e.min_x = block_reduce(mnx, MinOp(), S.red_u32);
+    e.max_x = block_reduce(mxx, MaxOp(), S.red_u32);
+    e.min_y = block_reduce(mny, MinOp(), S.red_u32);
+    e.max_y = block_reduce(mxy, MaxOp(), S.red_u32);
+    e.gx_sum = block_reduce(sgx, AddOp(), S.red_i32);
+    e.gy_sum = block_reduce(sgy, AddOp(), S.red_i32);
+    e.pg_sum = block_reduce(spg, AddOp(), S.red_i64);
+    e.count = n;
+    // ---- SelectBlobs (apriltag_gpu.cu:534-559); tag36h11: normal border only
+    bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
+    keep = keep && !((double)ext_dot(e) < 0.0);
+    if (!keep) continue;  // uniform across the workgroup
+    if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
+    const uint32_t bi = rank & 0xfff;
+
+    // ---- theta + sort key (P5/P6): (theta, dxy, y, x) -------------------------
+    const double cx = ext_cx(e), cy = ext_cy(e);
+    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+      const uint64_t k = S.u.keys[t];
+      const int dxy = (int)(k & 3);
+      const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
+      const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
+      const float dyf = (float)((double)py - cy);
+      const float dxf = (float)((double)px - cx);
+      const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
+      long long ti = (long long)rintf(theta);
+      if (ti < 0) ti = 0;
+      // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
+      S.u.keys[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
+                    ((uint64_t)bx << 1) | ((k >> 3) & 1);
+    }
+    int np2 = 64;
+    while (np2 < (int)n) np2 <<= 1;
+    for (int t = (int)n + tid; t < np2; t += kBlobThreads) S.u.keys[t] = ~0ull;
+    __syncthreads();
+    block_bitonic_sort<uint64_t, kBlobThreads>(S.u.keys, np2);
+
+    // ---- line-fit points + per-blob inclusive prefix sums (P7) -----------------
+    {
+      // Mx, My, W are int32 in the reference (LineFitPoint): wrap like two's complement
+      uint32_t cMx = 0, cMy = 0, cW = 0;
+      int64_t cMxx = 0, cMyy = 0, cMxy = 0;
+      for (uint32_t base = 0; base < n; base += kBlobThreads) {
+        const uint32_t t = base + tid;
+        uint32_t vMx = 0, vMy = 0, vW = 0;
+        int64_t vMxx = 0, vMyy = 0, vMxy = 0;
+        if (t < n) {
+          const uint64_t sk = S.u.keys[t];
+          const int dxy = (int)((sk >> 21) & 3);
+          const int32_t ix2 = (int32_t)(((sk >> 1) & 0x3ff) * 2 + dx_of(dxy)) + 1;
+          const int32_t iy2 = (int32_t)(((sk >> 11) & 0x3ff) * 2 + dy_of(dxy)) + 1;
+          const int32_t ix = ix2 / 2, iy = iy2 / 2;
+          int32_t Wt = 1;
+          if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
+            const int32_t gxv = (int32_t)dec[(size_t)iy * g.Wd + ix + 1] - (int32_t)dec[(size_t)iy * g.Wd + ix - 1];
+            const int32_t gyv = (int32_t)dec[(size_t)(iy + 1) * g.Wd + ix] - (int32_t)dec[(size_t)(iy - 1) * g.Wd + ix];
+            Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+          }
+          vMx = (uint32_t)(Wt * ix2); vMy = (uint32_t)(Wt * iy2); vW = (uint32_t)Wt;
+          vMxx = (int64_t)(Wt * ix2 * ix2); vMxy = (int64_t)(Wt * ix2 * iy2); vMyy = (int64_t)(Wt * iy2 * iy2);
+        }
+        uint32_t tot;
+        int64_t tot64;
+        const uint32_t pMx = block_incl_scan(vMx, S.red_u32, &tot) + cMx; cMx += tot;
+        const uint32_t pMy = block_incl_scan(vMy, S.red_u32, &tot) + cMy; cMy += tot;
+        const uint32_t pW = block_incl_scan(vW, S.red_u32, &tot) + cW; cW += tot;
+        int64_t pMxx = block_incl_scan(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
+        int64_t pMyy = block_incl_scan(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
+        int64_t pMxy = block_incl_scan(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
+        if (t < n) {
+          P.Mx[t] = (int32_t)pMx; P.My[t] = (int32_t)pMy; P.W[t] = (int32_t)pW;
+          P.Mxx[t] = pMxx; P.Myy[t] = pMyy; P.Mxy[t] = pMxy;
+          // debug tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
+          const uint64_t sk = S.u.keys[t];
+          const uint64_t pbits = (((sk >> 1) & 0x3ff) << 14) | (((sk >> 11) & 0x3ff) << 4) | ((sk & 1) << 3) |
+                                 ((sk >> 21) & 3);
+          grp[t] = ((uint64_t)bi << 52) | (((sk >> 23) & 0xfffffff) << 24) | pbits;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- errors, filter, peaks (K10 restated per blob, cyclic) ----------------
+    const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
+    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+      const uint32_t i0 = (t + 2 * n - ksz) % n, i1 = (t + n + ksz) % n;
+      const Moments m = read_moments(P, n, i0, i1);
+      const int64_t Wl = m.W;
+      const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
+      const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
+      const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
+      const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
+      const float eig = ((float)(Cxx + Cyy) - h) / (float)((double)(Wl * Wl) * 8.0);
+      P.err[t] = (double)((float)m.N * eig);
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+        const uint32_t idx = (uint32_t)((int64_t)t + j - 3 + n) % n;
+        acc += P.err[idx] * (double)c_filter[j];
+      }
+      P.filt[t] = acc;
+    }
+    if (tid == 0) S.npeaks = 0;
+    __syncthreads();
+    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+      const double me = P.filt[t];
+      const double bef = P.filt[(t + n - 1) % n], aft = P.filt[(t + 1) % n];
+      if (me > bef && me > aft) {
+        const float ef = (float)(-me);
+        uint32_t u = __float_as_uint(ef);
+        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // cub radix float order
+        const uint32_t slot = atomicAdd(&S.npeaks, 1u);
+        S.u.keys[slot] = ((uint64_t)u << 32) | t;
+      }
+    }
+    __syncthreads();
+    const uint32_t npk = S.npeaks;
+    {
+      int p2 = 2;
+      while (p2 < (int)npk) p2 <<= 1;
+      for (int t = (int)npk + tid; t < p2; t += kBlobThreads) S.u.keys[t] = ~0ull;
+      __syncthreads();
+      if (npk > 1) block_bitonic_sort<uint64_t, kBlobThreads>(S.u.keys, p2);
+    }
+    // ---- FitQuads (K11) --------------------------------------------------------
+    const int cnt = (int)npk;
+    if (tid == 0) {
+      int pi[16];
+      for (int t = 0; t < 16; t++)
+        pi[t] = (t < cnt && t < kNMaxima) ? (int)(S.u.keys[t] & 0xffffffffu) : 0xffff;
+      for (int a2 = 1; a2 < 16; a2++) {
+        const int v = pi[a2];
+        int c2 = a2 - 1;
+        while (c2 >= 0 && pi[c2] > v) { pi[c2 + 1] = pi[c2]; c2--; }
+        pi[c2 + 1] = v;
+      }
+      for (int t = 0; t < 16; t++) S.pi[t] = pi[t];
+    }
+    __syncthreads();
+    if (tid < 28) {
+      int m0 = 0, m1 = 0, c2 = 0;
+      for (int a2 = 0; a2 < 7; a2++)
+        for (int b2 = a2 + 1; b2 < 8; b2++) {
+          if (c2 == tid) { m0 = a2; m1 = b2; }
+          c2++;
+        }
+      if (cnt >= 4) {
+        if (m1 < kNMaxima && m1 < cnt) {
+          double err, mse;
+          fit_line(read_moments(P, n, S.pi[m0], S.pi[m1]), nullptr, S.lp01[m0][m1 - 1], &err, &mse);
+          if (mse > (double)prm.max_line_fit_mse) err = DBL_MAX;
+          S.e01[m0][m1 - 1] = err;
+        } else {
+          S.e01[m0][m1 - 1] = DBL_MAX;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 210) {
+      int m[4];
+      unrank(tid, m);
+      double err = DBL_MAX;
+      if (cnt >= 4 && m[3] < kNMaxima && m[3] < cnt && S.e01[m[0]][m[1] - 1] != DBL_MAX) {
+        double e12, mse12, p12[2];
+        fit_line(read_moments(P, n, S.pi[m[1]], S.pi[m[2]]), nullptr, p12, &e12, &mse12);
+        if (!(mse12 > (double)prm.max_line_fit_mse)) {
+          const double* p01 = S.lp01[m[0]][m[1] - 1];
+          const double dot = p01[0] * p12[0] + p01[1] * p12[1];
+          if (!(fabs(dot) > prm.cos_critical_rad)) {
+            double e23, mse23, e30, mse30;
+            fit_line(read_moments(P, n, S.pi[m[2]], S.pi[m[3]]), nullptr, nullptr, &e23, &mse23);
+            if (!(mse23 > (double)prm.max_line_fit_mse)) {
+              fit_line(read_moments(P, n, S.pi[m[3]], S.pi[m[0]]), nullptr, nullptr, &e30, &mse30);
+              if (!(mse30 > (double)prm.max_line_fit_mse)) err = S.e01[m[0]][m[1] - 1] + e12 + e23 + e30;
+            }
+          }
+        }
+      }
+      S.combo_err[tid] = err;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int bt = 0;
+      double best = S.combo_err[0];
+      for (int t = 1; t < 210; t++)
+        if (S.combo_err[t] < best) { best = S.combo_err[t]; bt = t; }
+      int m[4];
+      unrank(bt, m);
+      const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
+      QuadRecord rec;
+      rec.blob_index = bi;
+      rec.valid = valid;
+      rec.accepted = 0;
+      for (int k = 0; k < 4; k++) rec.indices[k] = (uint16_t)S.pi[m[k]];
+      int ok = 0;
+      if (valid) {
+        // UpdateFitQuads (apriltag_detect.cu:98-241)
+        double lines[4][4];
+        for (int k = 0; k < 4; k++) {
+          double err, mse;
+          fit_line(read_moments(P, n, rec.indices[k], rec.indices[(k + 1) & 3]), lines[k], lines[k] + 2, &err, &mse);
+        }
+        float qc[4][2];
+        ok = 1;
+        for (int k = 0; k < 4; k++) {
+          const int k1 = (k + 1) & 3;
+          const double A00 = lines[k][3], A01 = -lines[k1][3];
+          const double A10 = -lines[k][2], A11 = lines[k1][2];
+          const double B0 = -lines[k][0] + lines[k1][0];
+          const double B1 = -lines[k][1] + lines[k1][1];
+          const double det = A00 * A11 - A10 * A01;
+          const double W00 = A11 / det, W01 = -A01 / det;
+          if (fabs(det) < 0.001) { ok = 0; break; }
+          const double L0 = W00 * B0 + W01 * B1;
+          qc[k][0] = (float)(lines[k][0] + L0 * A00);
+          qc[k][1] = (float)(lines[k][1] + L0 * A10);
+        }
+        if (ok) {
+          float area = 0, len[3], pp;
+          for (int k = 0; k < 3; k++) {
+            const int a2 = k, b2 = (k + 1) % 3;
+            len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+          }
+          pp = (len[0] + len[1] + len[2]) / 2;
+          area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+          const int idxs[4] = {2, 3, 0, 2};
+          for (int k = 0; k < 3; k++) {
+            const int a2 = idxs[k], b2 = idxs[k + 1];
+            len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+          }
+          pp = (len[0] + len[1] + len[2]) / 2;
+          area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+          if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
+        }
+        if (ok) {
+          for (int k = 0; k < 4; k++) {
+            const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
+            const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
+            const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
+            const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
+            if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) { ok = 0; break; }
+          }
+        }
+        if (ok) {
+          for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
+            qc[k][0] = (qc[k][0] - 0.5f) * 2.0f + 0.5f;
+            qc[k][1] = (qc[k][1] - 0.5f) * 2.0f + 0.5f;
+            S.qc[k][0] = qc[k][0];
+            S.qc[k][1] = qc[k][1];
+            rec.corners[k][0] = qc[k][0];
+            rec.corners[k][1] = qc[k][1];
+          }
+        }
+      }
+      rec.accepted = ok;
+      if (!ok)
+        for (int k = 0; k < 4; k++) rec.corners[k][0] = rec.corners[k][1] = 0.f;
+      const uint32_t qi = atomicAdd(b.nquads + f, 1u);
+      if (qi < (uint32_t)kMaxQuads) b.quads[(size_t)f * kMaxQuads + qi] = rec;
+      S.ok = ok;
+    }
+    __syncthreads();
+    if (!S.ok) continue;
+
+    // ---- RefineEdges (apriltag_detect.cu:405-564) -----------------------------
+    if (prm.refine_edges) {
+      if (tid < 4) {
+        const int a2 = tid, b2 = (tid + 1) & 3;
+        float nx = S.qc[b2][1] - S.qc[a2][1];
+        float ny = -S.qc[b2][0] + S.qc[a2][0];
+        const float mag = sqrtf(nx * nx + ny * ny);
+        nx /= mag;
+        ny /= mag;
+        const int nsf = (int)(mag / 8);
+        S.nsamp[tid] = nsf > 16 ? nsf : 16;
+        S.enx[tid] = nx;
+        S.eny[tid] = ny;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int acc = 0;
+        for (int k = 0; k < 4; k++) {
+          S.samp_off[k] = acc;
+          acc += S.nsamp[k];
+        }
+      }
+      __syncthreads();
+      const int total = S.samp_off[3] + S.nsamp[3];
+      const int cap = kSortCap / 2;
+      for (int t = tid; t < total && t < cap; t += kBlobThreads) {
+        int edge = 0;
+        while (edge < 3 && t >= S.samp_off[edge + 1]) edge++;
+        const int s = t - S.samp_off[edge];
+        const int a2 = edge, b2 = (edge + 1) & 3;
+        const int nsamples = S.nsamp[edge];
+        const float nx = S.enx[edge], ny = S.eny[edge];
+        const double alpha = (1.0 + s) / (nsamples + 1);
+        const double x0 = alpha * S.qc[a2][0] + (1 - alpha) * S.qc[b2][0];
+        const double y0 = alpha * S.qc[a2][1] + (1 - alpha) * S.qc[b2][1];
+        double Mn = 0, Mcount = 0;
+        const double range = 3.0;
+        for (double nn = -range; nn <= range; nn += 0.25) {
+          const double grange = 1;
+          const int x1 = (int)(x0 + (nn + grange) * nx);
+          const int y1 = (int)(y0 + (nn + grange) * ny);
+          if (x1 < 0 || x1 >= g.W || y1 < 0 || y1 >= g.H) continue;
+          const int x2 = (int)(x0 + (nn - grange) * nx);
+          const int y2 = (int)(y0 + (nn - grange) * ny);
+          if (x2 < 0 || x2 >= g.W || y2 < 0 || y2 >= g.H) continue;
+          const int g1 = gray[(size_t)y1 * g.W + x1], g2 = gray[(size_t)y2 * g.W + x2];
+          if (g1 < g2) continue;
+          const double weight = (double)((g2 - g1) * (g2 - g1));
+          Mn += weight * nn;
+          Mcount += weight;
+        }
+        double bx = __longlong_as_double(0x7ff8deadbeef0000ll), by = 0;
+        if (Mcount != 0) {
+          const double n0 = Mn / Mcount;
+          bx = x0 + n0 * nx;
+          by = y0 + n0 * ny;
+          undistort(prm, &bx, &by);
+        }
+        S.u.smp.sx[t] = bx;
+        S.u.smp.sy[t] = by;
+      }
+      __syncthreads();
+      if (tid < 4) {
+        double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
+        const int o = S.samp_off[tid];
+        for (int s = 0; s < S.nsamp[tid] && o + s < cap; s++) {
+          const double bx = S.u.smp.sx[o + s], by = S.u.smp.sy[o + s];
+          if (isnan(bx)) continue;
+          Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
+        }
+        const double Ex = Mx / N, Ey = My / N;
+        const double Cxx = Mxx / N - Ex * Ex, Cxy = Mxy / N - Ex * Ey, Cyy = Myy / N - Ey * Ey;
+        const double nt = .5 * (double)det_atan2f((float)(-2 * Cxy), (float)(Cyy - Cxx));
+        S.lines[tid][0] = Ex;
+        S.lines[tid][1] = Ey;
+        S.lines[tid][2] = (double)det_cosf((float)nt);
+        S.lines[tid][3] = (double)det_sinf((float)nt);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float qp[4][2];
+        for (int k = 0; k < 4; k++) { qp[k][0] = S.qc[k][0]; qp[k][1] = S.qc[k][1]; }
+        for (int i = 0; i < 4; i++) {
+          const int i1 = (i + 1) & 3;
+          const double A00 = S.lines[i][3], A01 = -S.lines[i1][3];
+          const double A10 = -S.lines[i][2], A11 = S.lines[i1][2];
+          const double B0 = -S.lines[i][0] + S.lines[i1][0];
+          const double B1 = -S.lines[i][1] + S.lines[i1][1];
+          const double det = A00 * A11 - A10 * A01;
+          if (fabs(det) > 0.001) {
+            const double W00 = A11 / det, W01 = -A01 / det;
+            const double L0 = W00 * B0 + W01 * B1;
+            double px = S.lines[i][0] + L0 * A00, py = S.lines[i][1] + L0 * A10;
+            redistort(prm, &px, &py);
+            qp[i1][0] = (float)px;
+            qp[i1][1] = (float)py;
+          }
+        }
+        for (int k = 0; k < 4; k++) { S.qc[k][0] = qp[k][0]; S.qc[k][1] = qp[k][1]; }
+      }
+      __syncthreads();
+    }
+    // ---- homography (quad_update_homographies / homography_compute2) -----------
+    if (tid == 0) {
+      double corr[4][4];
+      for (int i = 0; i < 4; i++) {
+        corr[i][0] = (i == 0 || i == 3) ? -1 : 1;
+        corr[i][1] = (i == 0 || i == 1) ? -1 : 1;
+        corr[i][2] = S.qc[i][0];
+        corr[i][3] = S.qc[i][1];
+      }
+      double H[9];
+      int okh = homography_compute2(corr, H) == 0;
+      if (okh) {
+        const double hdet = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                            H[2] * (H[3] * H[7] - H[4] * H[6]);
+        okh = hdet != 0;
+      }
+      for (int k = 0; k < 9; k++) S.H[k] = H[k];
+      S.ok = okh;
+    }
+    __syncthreads();
+    if (!S.ok) continue;
+    // ---- quad_decode: border gray models ----------------------------------------
+    if (tid < 64) {
+      const int pidx = tid >> 3, i = tid & 7;
+      const float wab = 8.0f;
+      const float pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0, 1, 0}, {wab + 0.5f, .5f, 0, 1, 1},
+                               {wab - 0.5f, .5f, 0, 1, 0}, {0.5f, -0.5f, 1, 0, 1}, {0.5f, 0.5f, 1, 0, 0},
+                               {0.5f, wab + 0.5f, 1, 0, 1}, {0.5f, wab - 0.5f, 1, 0, 0}};
+      const double tagx01 = (double)((pat[pidx][0] + (float)i * pat[pidx][2]) / 8.0f);
+      const double tagy01 = (double)((pat[pidx][1] + (float)i * pat[pidx][3]) / 8.0f);
+      const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
+      double px, py;
+      hproject(S.H, tagx, tagy, &px, &py);
+      const int ix = (int)px, iy = (int)py;
+      S.gmx[tid] = tagx;
+      S.gmy[tid] = tagy;
+      S.gmvalid[tid] = !(ix < 0 || iy < 0 || ix >= g.W || iy >= g.H);
+      S.gmv[tid] = S.gmvalid[tid] ? (double)gray[(size_t)iy * g.W + ix] : 0.0;
+    }
+    for (int t = tid; t < 100; t += kBlobThreads) S.values[t] = 0;
+    __syncthreads();
+    GrayModel wm, bm;
+    if (tid == 0) {
+      for (int k = 0; k < 3; k++) {
+        wm.B[k] = bm.B[k] = 0;
+        for (int j = 0; j < 3; j++) wm.A[k][j] = bm.A[k][j] = 0;
+      }
+      for (int t = 0; t < 64; t++) {
+        if (!S.gmvalid[t]) continue;
+        const int is_white = ((t >> 3) & 1) == 0;
+        if (is_white) gm_add(wm, S.gmx[t], S.gmy[t], S.gmv[t]);
+        else gm_add(bm, S.gmx[t], S.gmy[t], S.gmv[t]);
+      }
+      gm_solve(wm);
+      gm_solve(bm);
+      S.ok = !(gm_interp(wm, 0, 0) - gm_interp(bm, 0, 0) < 0);
+      for (int k = 0; k < 3; k++) {
+        S.red_f64[k] = wm.C[k];
+        S.lines[0][k] = bm.C[k];
+      }
+    }
+    __syncthreads();
+    if (!S.ok) continue;
+    if (tid < 36) {
+      const int bity = c_bity[tid], bitx = c_bitx[tid];
+      const double tagx01 = (bitx + 0.5) / 8, tagy01 = (bity + 0.5) / 8;
+      const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
+      double px, py;
+      hproject(S.H, tagx, tagy, &px, &py);
+      // value_for_pixel (bilinear)
+      const int x1 = (int)floor(px - 0.5), x2 = (int)ceil(px - 0.5);
+      const double xx = px - 0.5 - x1;
+      const int y1 = (int)floor(py - 0.5), y2 = (int)ceil(py - 0.5);
+      const double yy = py - 0.5 - y1;
+      if (!(x1 < 0 || x2 >= g.W || y1 < 0 || y2 >= g.H)) {
+        const double v = gray[(size_t)y1 * g.W + x1] * (1 - xx) * (1 - yy) + gray[(size_t)y1 * g.W + x2] * xx * (1 - yy) +
+                         gray[(size_t)y2 * g.W + x1] * (1 - xx) * yy + gray[(size_t)y2 * g.W + x2] * xx * yy;
+        const double bth = S.lines[0][0] * tagx + S.lines[0][1] * tagy + S.lines[0][2];
+        const double wth = S.red_f64[0] * tagx + S.red_f64[1] * tagy + S.red_f64[2];
+        const double thresh = (bth + wth) / 2.0;
+        S.values[10 * (bity + 1) + bitx + 1] = v - thresh;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double sh[100];
+      const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
+      for (int y = 0; y < 10; y++)
+        for (int x = 0; x < 10; x++) {
+          sh[y * 10 + x] = 0;
+          for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+              if ((y + i - 1) < 0 || (y + i - 1) > 9 || (x + j - 1) < 0 || (x + j - 1) > 9) continue;
+              sh[y * 10 + x] += S.values[(y + i - 1) * 10 + (x + j - 1)] * kern[i * 3 + j];
+            }
+        }
+      for (int t = 0; t < 100; t++) S.values[t] = S.values[t] + prm.decode_sharpening * sh[t];
+      float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
+      uint64_t rcode = 0;
+      for (int i = 0; i < 36; i++) {
+        rcode = rcode << 1;
+        const double v = S.values[10 * (c_bity[i] + 1) + c_bitx[i] + 1];
+        if (v > 0) { white_score = (float)(white_score + v); white_cnt++; rcode |= 1; }
+        else { black_score = (float)(black_score - v); black_cnt++; }
+      }
+      S.red_u64[0] = rcode;
+      S.red_f64[3] = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
+      S.best_code = 0xffffffffu;
+    }
+    __syncthreads();
+    {
+      // quick_decode_codeword: first rotation (then entry) within hamming <= 2
+      const uint64_t rcode = S.red_u64[0];
+      for (int t = tid; t < 4 * c_book.n; t += kBlobThreads) {
+        const int rot = t / c_book.n, ent = t % c_book.n;
+        uint64_t r = rcode;
+        for (int k = 0; k < rot; k++) r = rotate90_36(r);
+        const int hd = __popcll(r ^ c_book.code[ent]);
+        if (hd <= 2) atomicMin(&S.best_code, (uint32_t)((rot << 24) | (hd << 16) | ent));
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float margin = (float)S.red_f64[3];
+      const uint32_t bc = S.best_code;
+      if (margin >= 0 && bc != 0xffffffffu) {
+        const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
+        DevDetection d;
+        d.id = c_book.id[ent];
+        d.hamming = hd;
+        d.decision_margin = margin;
+        d.blob_rank = (int32_t)rank;
+        const double kRotC[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
+        const double kRotS[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
+        const double R[9] = {kRotC[rot], -kRotS[rot], 0, kRotS[rot], kRotC[rot], 0, 0, 0, 1};
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += S.H[i * 3 + k] * R[k * 3 + j];
+            d.H[i * 3 + j] = acc;
+          }
+        hproject(d.H, 0, 0, &d.c[0], &d.c[1]);
+        for (int i = 0; i < 4; i++) {
+          const int tcx = (i == 1 || i == 2) ? 1 : -1;
+          const int tcy = (i < 2) ? 1 : -1;
+          hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
+        }
+        const uint32_t di = atomicAdd(b.ndets + f, 1u);
+        if (di < (uint32_t)kMaxDets) b.dets[(size_t)f * kMaxDets + di] = d;
+        else atomicOr(b.status + f, kStatusDetsOverflow);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers (called from at_api.cpp)
+// ---------------------------------------------------------------------------
+hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
+  DevCodebook cb;
+  cb.n = n;
+  for (int i = 0; i < n && i < 96; i++) {
+    cb.code[i] = codes[i];
+    cb.id[i] = ids[i];
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_book), &cb, sizeof(cb));
+}
+
+hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
+                           hipStream_t st) {
+  {
+    dim3 blk(64, 4), grd((g.TW + 63) / 64, (g.TH + 3) / 4, B);
+    if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
+    else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
+    else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
+  }
+  {
+    dim3 grd(g.CTX, g.CTY, B);
+    hipLaunchKernelGGL(k_thr_ccl, grd, dim3(256), 0, st, b, g, prm);
+    hipLaunchKernelGGL(k_ccl_border, grd, dim3(64), 0, st, b, g);
+  }
+  {
+    dim3 blk(64, 4), grd((g.BW + 63) / 64, (g.BH + 3) / 4, B);
+    hipLaunchKernelGGL(k_ccl_final, grd, blk, 0, st, b, g);
+  }
+  {
+    dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 3) / 4, B);
+    hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
+  }
+  hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g);
+  hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
+  hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
+  return hipGetLastError();
+}
+
+}  // namespace at

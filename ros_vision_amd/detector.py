@@ -1,0 +1,301 @@
+"""Python mirror of the reference detector interface over the C ABI.
+
+``GpuDetector`` follows frc971::apriltag::GpuDetector
+(src/apriltags_cuda/include/apriltags_cuda/apriltag_gpu.h:77-359): construct
+once per camera with width, height and calibration, call ``detect(frame)``
+per frame, read ``detections()``; the debug copy-outs
+(apriltag_gpu.h:98-183) are the ``copy_*`` methods.  Everything runs in
+``libat_hip.so`` (HIP kernels for gfx950); there is no CPU fallback: if the
+library or a GPU is missing the constructor raises.
+"""
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libat_hip.so")
+
+AT_FMT_YUYV, AT_FMT_BGR8, AT_FMT_GRAY8 = 0, 1, 2
+(AT_STAGE_GRAY, AT_STAGE_DECIMATED, AT_STAGE_THRESHOLD, AT_STAGE_LABELS, AT_STAGE_SIZES,
+ AT_STAGE_NUM_POINTS, AT_STAGE_NUM_PAIRS, AT_STAGE_QUADS, AT_STAGE_POINTS, AT_STAGE_BLOB_POINTS) = range(10)
+AT_E_CAPACITY = -3
+
+# Symbols declared in include/at_api.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "at_config_default", "at_create", "at_detect", "at_detect_batch", "at_detect_device",
+    "at_enqueue_device", "at_collect", "at_frame_status", "at_debug_copy", "at_destroy",
+    "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
+]
+
+
+class AtConfig(C.Structure):
+    _fields_ = [
+        ("width", C.c_int), ("height", C.c_int), ("family", C.c_char_p),
+        ("quad_decimate", C.c_float), ("refine_edges", C.c_int), ("decode_sharpening", C.c_double),
+        ("min_white_black_diff", C.c_int), ("min_cluster_pixels", C.c_int), ("max_nmaxima", C.c_int),
+        ("max_line_fit_mse", C.c_float), ("cos_critical_rad", C.c_double),
+        ("device", C.c_int), ("max_batch", C.c_int),
+    ]
+
+
+class AtCamera(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3")]
+
+
+class AtDetection(C.Structure):
+    _fields_ = [
+        ("id", C.c_int32), ("hamming", C.c_int32), ("decision_margin", C.c_float),
+        ("H", C.c_double * 9), ("c", C.c_double * 2), ("p", (C.c_double * 2) * 4),
+    ]
+
+
+class AtQuadRecord(C.Structure):
+    _fields_ = [
+        ("blob_index", C.c_uint32), ("valid", C.c_uint32), ("accepted", C.c_uint32),
+        ("indices", C.c_uint16 * 4), ("corners", (C.c_float * 2) * 4),
+    ]
+
+
+@dataclass
+class Detection:
+    """apriltag_detection_t fields the node consumes (apriltags_cuda_detector.cu:425-496)."""
+    id: int
+    hamming: int
+    decision_margin: float
+    H: np.ndarray
+    c: np.ndarray
+    p: np.ndarray
+
+
+@dataclass
+class CameraMatrix:
+    """apriltag_gpu.h:61-66"""
+    fx: float
+    cx: float
+    fy: float
+    cy: float
+
+
+@dataclass
+class DistCoeffs:
+    """apriltag_gpu.h:68-74"""
+    k1: float
+    k2: float
+    p1: float
+    p2: float
+    k3: float
+
+
+# Intrinsics the reference's own test uses (test/gpu_detector_test.cu:62-73).
+TEST_CAMERA = CameraMatrix(fx=905.495617, cx=609.916016, fy=907.909470, cy=352.682645)
+TEST_DIST = DistCoeffs(k1=0.059238, k2=-0.075154, p1=-0.003801, p2=0.001113, k3=0.0)
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libat_hip.so; raises if it is missing (no CPU fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError("libat_hip.so not built: run `make -C ros_vision_amd/csrc` "
+                           "(or __graft_entry__.build())")
+    L = C.CDLL(path)
+    L.at_config_default.argtypes = [C.POINTER(AtConfig), C.c_int, C.c_int]
+    L.at_create.argtypes = [C.POINTER(AtConfig), C.POINTER(AtCamera), C.POINTER(C.c_void_p)]
+    L.at_detect.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(AtDetection), C.c_int, C.POINTER(C.c_int)]
+    L.at_detect_batch.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(AtDetection),
+                                  C.c_int, C.POINTER(C.c_int)]
+    L.at_detect_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(AtDetection),
+                                   C.c_int, C.POINTER(C.c_int)]
+    L.at_enqueue_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]
+    L.at_collect.argtypes = [C.c_void_p, C.POINTER(AtDetection), C.c_int, C.POINTER(C.c_int)]
+    L.at_frame_status.argtypes = [C.c_void_p, C.c_int]
+    L.at_debug_copy.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
+    L.at_debug_copy.restype = C.c_longlong
+    L.at_destroy.argtypes = [C.c_void_p]
+    L.at_strerror.restype = C.c_char_p
+    L.at_strerror.argtypes = [C.c_int]
+    L.at_family_num_known.argtypes = [C.c_char_p]
+    L.at_family_entry.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+    _LIB = L
+    return L
+
+
+def family_entries(family: str = "tag36h11"):
+    """(id, code) pairs of the codewords known to the library."""
+    L = load_library()
+    n = L.at_family_num_known(family.encode())
+    out = []
+    for i in range(n):
+        tid, code = C.c_int(), C.c_uint64()
+        L.at_family_entry(family.encode(), i, C.byref(tid), C.byref(code))
+        out.append((tid.value, code.value))
+    return out
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise RuntimeError("%s failed: %s (%d)" % (what, load_library().at_strerror(rc).decode(), rc))
+    return rc
+
+
+class GpuDetector:
+    """Drop-in for frc971::apriltag::GpuDetector on MI355X (one instance per camera)."""
+
+    MAX_DETECTIONS = 128
+
+    def __init__(self, width, height, camera_matrix: CameraMatrix = TEST_CAMERA,
+                 distortion_coefficients: DistCoeffs = TEST_DIST, family="tag36h11",
+                 max_batch=1, device=0, **overrides):
+        L = load_library()
+        self.width, self.height, self.max_batch = int(width), int(height), int(max_batch)
+        cfg = AtConfig()
+        L.at_config_default(C.byref(cfg), self.width, self.height)
+        self._family = family.encode()
+        cfg.family = self._family
+        cfg.max_batch = self.max_batch
+        cfg.device = int(device)
+        for k, v in overrides.items():
+            setattr(cfg, k, v)
+        cam = AtCamera(fx=camera_matrix.fx, fy=camera_matrix.fy, cx=camera_matrix.cx, cy=camera_matrix.cy,
+                       k1=distortion_coefficients.k1, k2=distortion_coefficients.k2,
+                       p1=distortion_coefficients.p1, p2=distortion_coefficients.p2,
+                       k3=distortion_coefficients.k3)
+        h = C.c_void_p()
+        _check(L.at_create(C.byref(cfg), C.byref(cam), C.byref(h)), "at_create")
+        self._h = h
+        self._cap = self.MAX_DETECTIONS
+        self._out = (AtDetection * (self._cap * self.max_batch))()
+        self._n = (C.c_int * self.max_batch)()
+        self._last = [[] for _ in range(self.max_batch)]
+        self._last_status = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().at_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- detection ---------------------------------------------------------
+    def _unpack(self, nframes):
+        res = []
+        for f in range(nframes):
+            dets = []
+            for i in range(min(self._n[f], self._cap)):
+                d = self._out[f * self._cap + i]
+                dets.append(Detection(id=d.id, hamming=d.hamming, decision_margin=d.decision_margin,
+                                      H=np.array(list(d.H)).reshape(3, 3), c=np.array(list(d.c)),
+                                      p=np.array([[d.p[k][0], d.p[k][1]] for k in range(4)])))
+            res.append(dets)
+        self._last = res
+        return res
+
+    def detect(self, frame: np.ndarray, fmt: int = AT_FMT_YUYV):
+        """GpuDetector::Detect (apriltag_gpu.cu:725): one host frame, synchronous."""
+        frame = np.ascontiguousarray(frame, dtype=np.uint8)
+        rc = load_library().at_detect(self._h, frame.ctypes.data, fmt, self._out, self._cap, self._n)
+        self._last_status = rc
+        if rc < 0 and rc != AT_E_CAPACITY:
+            _check(rc, "at_detect")
+        return self._unpack(1)[0]
+
+    def detect_batch(self, frames, fmt: int = AT_FMT_YUYV):
+        frames = [np.ascontiguousarray(f, dtype=np.uint8) for f in frames]
+        ptrs = (C.c_void_p * len(frames))(*[f.ctypes.data for f in frames])
+        rc = load_library().at_detect_batch(self._h, ptrs, len(frames), fmt, self._out, self._cap, self._n)
+        self._last_status = rc
+        if rc < 0 and rc != AT_E_CAPACITY:
+            _check(rc, "at_detect_batch")
+        return self._unpack(len(frames))
+
+    def detect_device(self, dev_ptr: int, frame_stride: int, nframes: int, fmt: int = AT_FMT_YUYV):
+        """Frames already resident in device memory (e.g. a torch.cuda tensor's data_ptr())."""
+        rc = load_library().at_detect_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt,
+                                             self._out, self._cap, self._n)
+        self._last_status = rc
+        if rc < 0 and rc != AT_E_CAPACITY:
+            _check(rc, "at_detect_device")
+        return self._unpack(nframes)
+
+    def enqueue_device(self, dev_ptr: int, frame_stride: int, nframes: int, fmt: int = AT_FMT_YUYV):
+        _check(load_library().at_enqueue_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt),
+               "at_enqueue_device")
+        self._pending = nframes
+
+    def collect(self):
+        rc = load_library().at_collect(self._h, self._out, self._cap, self._n)
+        if rc < 0 and rc != AT_E_CAPACITY:
+            _check(rc, "at_collect")
+        return self._unpack(self._pending)
+
+    def detections(self, frame=0):
+        """GpuDetector::Detections (apriltag_gpu.h:93), sorted by id."""
+        return self._last[frame]
+
+    def frame_status(self, frame=0):
+        return load_library().at_frame_status(self._h, frame)
+
+    # ---- parity taps (apriltag_gpu.h:98-183) -------------------------------
+    def _copy(self, stage, frame, nbytes, dtype):
+        buf = np.empty(nbytes // np.dtype(dtype).itemsize, dtype=dtype)
+        n = load_library().at_debug_copy(self._h, stage, frame, buf.ctypes.data, buf.nbytes)
+        _check(int(n), "at_debug_copy")
+        return buf[: n // np.dtype(dtype).itemsize]
+
+    def copy_gray(self, frame=0):
+        return self._copy(AT_STAGE_GRAY, frame, self.width * self.height, np.uint8).reshape(self.height, self.width)
+
+    def copy_decimated(self, frame=0):
+        return self._copy(AT_STAGE_DECIMATED, frame, self.width * self.height // 4,
+                          np.uint8).reshape(self.height // 2, self.width // 2)
+
+    def copy_thresholded(self, frame=0):
+        return self._copy(AT_STAGE_THRESHOLD, frame, self.width * self.height // 4,
+                          np.uint8).reshape(self.height // 2, self.width // 2)
+
+    def copy_union_markers(self, frame=0):
+        return self._copy(AT_STAGE_LABELS, frame, self.width * self.height,
+                          np.uint32).reshape(self.height // 2, self.width // 2)
+
+    def copy_union_markers_size(self, frame=0):
+        return self._copy(AT_STAGE_SIZES, frame, self.width * self.height, np.uint32)
+
+    def num_points(self, frame=0):
+        return int(self._copy(AT_STAGE_NUM_POINTS, frame, 4, np.uint32)[0])
+
+    def num_pairs(self, frame=0):
+        return int(self._copy(AT_STAGE_NUM_PAIRS, frame, 4, np.uint32)[0])
+
+    def copy_points(self, frame=0):
+        """Boundary points (QuadBoundaryPoint keys), device emission order."""
+        return self._copy(AT_STAGE_POINTS, frame, 8 * max(1, self.num_points(frame)), np.uint64)
+
+    def copy_blob_points(self, frame=0):
+        """IndexPoint keys of the selected blobs in (blob, theta, plane, y, x) order."""
+        L = load_library()
+        need = L.at_debug_copy(self._h, AT_STAGE_BLOB_POINTS, frame, C.c_void_p(1), 0)
+        need = max(int(need), 8)
+        return self._copy(AT_STAGE_BLOB_POINTS, frame, need, np.uint64)
+
+    def copy_quads(self, frame=0):
+        recs = (AtQuadRecord * 512)()
+        n = load_library().at_debug_copy(self._h, AT_STAGE_QUADS, frame, C.cast(recs, C.c_void_p), C.sizeof(recs))
+        _check(int(n), "at_debug_copy")
+        out = []
+        for i in range(int(n) // C.sizeof(AtQuadRecord)):
+            r = recs[i]
+            out.append(dict(blob_index=r.blob_index, valid=bool(r.valid), accepted=bool(r.accepted),
+                            indices=list(r.indices),
+                            corners=np.array([[r.corners[k][0], r.corners[k][1]] for k in range(4)], np.float32)))
+        return out
+
+
+def default_cos_critical_rad():
+    return math.cos(10.0 * math.pi / 180.0)

@@ -1,0 +1,121 @@
+"""Seeded synthetic tag36h11 boards.
+
+A frame is a mid-gray background with ``ntags`` tag36h11 tags on a jittered
+grid; each tag gets a random side length, rotation and perspective
+(corner jitter), is rendered with bilinear interpolation from a 10x10-cell
+bitmap (white quiet zone, black border, 6x6 data cells in the apriltag 3.x
+bit layout) and the frame gets Gaussian noise.  Output is the gray plane or
+packed YUYV with U = V = 128 (what cvtColor(BGR2YUV_YUYV) produces for a gray
+image, apriltags_cuda_detector.cu:401).  Only ids whose codeword is known
+offline are used (codebook).
+"""
+import numpy as np
+
+# tag36h11 bit layout (apriltag 3.x), data cells in border coordinates 1..6
+BIT_X = [1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3]
+BIT_Y = [1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4]
+
+
+def tag_cells(code: int) -> np.ndarray:
+    """10x10 cell image (1 = white) of a tag36h11 codeword incl. the quiet zone."""
+    cells = np.ones((10, 10), np.float32)
+    cells[1:9, 1:9] = 0.0  # black border ring
+    for i in range(36):
+        if (code >> (35 - i)) & 1:
+            cells[BIT_Y[i] + 1, BIT_X[i] + 1] = 1.0
+    return cells
+
+
+def homography(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    A = []
+    for (x, y), (u, v) in zip(src, dst):
+        A.append([x, y, 1, 0, 0, 0, -u * x, -u * y, -u])
+        A.append([0, 0, 0, x, y, 1, -v * x, -v * y, -v])
+    _, _, vt = np.linalg.svd(np.asarray(A, np.float64))
+    Hm = vt[-1].reshape(3, 3)
+    return Hm / Hm[2, 2]
+
+
+def _known_ids():
+    from .detector import family_entries  # codebook lives in the C library
+    return sorted(i for i, _ in family_entries())
+
+
+def _codes():
+    from .detector import family_entries
+    return dict(family_entries())
+
+
+def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigma: float = 2.0,
+                 side_range=(64, 128), ids=None, background: int = 128, codes=None):
+    """Render one gray frame; returns (gray uint8 [H,W], list of (id, corners[4,2]))."""
+    rng = np.random.default_rng(seed)
+    codes = codes if codes is not None else _codes()
+    known = sorted(codes)
+    if ids is None:
+        start = int(rng.integers(0, len(known)))
+        ids = [known[(start + j) % len(known)] for j in range(ntags)]
+    img = np.full((height, width), float(background), np.float32)
+    rows = int(np.floor(np.sqrt(ntags * height / width))) or 1
+    cols = int(np.ceil(ntags / rows))
+    cw, ch = width / cols, height / rows
+    truth = []
+    sup = 8  # bitmap pixels per cell
+    for j, tid in enumerate(ids):
+        r, c = divmod(j, cols)
+        side = float(rng.uniform(*side_range))
+        side = min(side, 0.8 * min(cw, ch))
+        cx = (c + 0.5) * cw + rng.uniform(-0.08, 0.08) * cw
+        cy = (r + 0.5) * ch + rng.uniform(-0.08, 0.08) * ch
+        ang = np.deg2rad(rng.uniform(-10, 10))
+        # square of the full 10-cell tag (quiet zone included), then perspective jitter
+        half = side / 2 * 10 / 8
+        base = np.array([[-half, -half], [half, -half], [half, half], [-half, half]])
+        rot = np.array([[np.cos(ang), -np.sin(ang)], [np.sin(ang), np.cos(ang)]])
+        corners = base @ rot.T + np.array([cx, cy])
+        corners += rng.uniform(-0.15, 0.15, size=(4, 2)) * half * 0.5
+        src = np.array([[0, 0], [10, 0], [10, 10], [0, 10]], np.float64)
+        Hm = homography(src, corners)
+        Hinv = np.linalg.inv(Hm)
+        bmp = np.kron(tag_cells(codes[tid]), np.ones((sup, sup), np.float32)) * 255.0
+        x0, y0 = np.floor(corners.min(0)).astype(int) - 1
+        x1, y1 = np.ceil(corners.max(0)).astype(int) + 1
+        x0, y0, x1, y1 = max(x0, 0), max(y0, 0), min(x1, width - 1), min(y1, height - 1)
+        xs, ys = np.meshgrid(np.arange(x0, x1 + 1), np.arange(y0, y1 + 1))
+        pts = np.stack([xs.ravel() + 0.5, ys.ravel() + 0.5, np.ones(xs.size)])
+        tp = Hinv @ pts
+        u, v = tp[0] / tp[2], tp[1] / tp[2]
+        inside = (u >= 0) & (u < 10) & (v >= 0) & (v < 10)
+        bu, bv = u * sup - 0.5, v * sup - 0.5
+        iu = np.clip(np.floor(bu).astype(int), 0, 10 * sup - 2)
+        iv = np.clip(np.floor(bv).astype(int), 0, 10 * sup - 2)
+        fu = np.clip(bu - iu, 0, 1)
+        fv = np.clip(bv - iv, 0, 1)
+        val = (bmp[iv, iu] * (1 - fu) * (1 - fv) + bmp[iv, iu + 1] * fu * (1 - fv) +
+               bmp[iv + 1, iu] * (1 - fu) * fv + bmp[iv + 1, iu + 1] * fu * fv)
+        flat = img[y0:y1 + 1, x0:x1 + 1].ravel()
+        flat[inside] = val[inside]
+        img[y0:y1 + 1, x0:x1 + 1] = flat.reshape(ys.shape)
+        # tag black-border corners (cells 1 and 9) in image space
+        bc = np.array([[1, 1], [9, 1], [9, 9], [1, 9]], np.float64)
+        hb = Hm @ np.vstack([bc.T, np.ones(4)])
+        truth.append((tid, (hb[:2] / hb[2]).T))
+    if noise_sigma > 0:
+        img += rng.normal(0.0, noise_sigma, size=img.shape).astype(np.float32)
+    gray = np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    return gray, truth
+
+
+def to_yuyv(gray: np.ndarray) -> np.ndarray:
+    """Pack a gray plane as YUYV 4:2:2 (Y0 U Y1 V) with U = V = 128."""
+    h, w = gray.shape
+    out = np.empty((h, 2 * w), np.uint8)
+    out[:, 0::2] = gray
+    out[:, 1::2] = 128
+    return out
+
+
+def stream_frame(width: int, height: int, frame: int, camera: int = 0, ntags: int = 15, codes=None):
+    """Config C2/C3 frame: seed 766000 + frame (+ camera * 10**6)."""
+    gray, truth = render_board(width, height, seed=766000 + frame + camera * 10 ** 6, ntags=ntags, codes=codes)
+    return to_yuyv(gray), gray, truth

@@ -1,0 +1,57 @@
+"""Helpers comparing the HIP path (C ABI) with the CPU oracle stage by stage."""
+import numpy as np
+
+
+def compare_frame(det, orc, frame_idx=0, check_points=True):
+    """Returns a list of mismatch descriptions (empty == bit-identical)."""
+    bad = []
+    for name, a, b in [("gray", det.copy_gray(frame_idx), orc.gray()),
+                       ("decimated", det.copy_decimated(frame_idx), orc.decimated()),
+                       ("threshold", det.copy_thresholded(frame_idx), orc.thresholded()),
+                       ("labels", det.copy_union_markers(frame_idx), orc.labels()),
+                       ("sizes", det.copy_union_markers_size(frame_idx), orc.sizes())]:
+        if a.shape != b.shape or not np.array_equal(a, b):
+            nd = int(np.count_nonzero(a != b)) if a.shape == b.shape else -1
+            bad.append("%s differs at %d positions" % (name, nd))
+            return bad  # later stages depend on these
+    if check_points:
+        gp = np.sort(det.copy_points(frame_idx))
+        op = np.sort(orc.sorted_points())
+        if not np.array_equal(gp, op):
+            bad.append("boundary points differ: gpu %d oracle %d" % (gp.size, op.size))
+            return bad
+    if det.num_pairs(frame_idx) != orc.num_pairs():
+        bad.append("pairs %d vs %d" % (det.num_pairs(frame_idx), orc.num_pairs()))
+    gb = det.copy_blob_points(frame_idx)
+    ob = orc.sorted_index_points()
+    if gb.shape != ob.shape or not np.array_equal(gb, ob):
+        nd = int(np.count_nonzero(gb != ob)) if gb.shape == ob.shape else -1
+        bad.append("selected blob points differ (gpu %d oracle %d, %d mismatches)" % (gb.size, ob.size, nd))
+    gq = [q for q in det.copy_quads(frame_idx) if q["valid"]]
+    oq = [f for f in orc.fitquads() if f.valid]
+    gqi = [(q["blob_index"], tuple(q["indices"])) for q in gq]
+    oqi = [(int(f.blob_index), tuple(int(v) for v in f.indices)) for f in oq]
+    if gqi != oqi:
+        bad.append("valid fit quads differ: %s vs %s" % (gqi[:5], oqi[:5]))
+    ga = [(q["blob_index"], q["corners"].tobytes()) for q in det.copy_quads(frame_idx) if q["accepted"]]
+    oa = [(b, c.tobytes()) for c, b in orc.quads()]
+    if ga != oa:
+        bad.append("accepted quad corners differ (%d vs %d)" % (len(ga), len(oa)))
+    return bad
+
+
+def compare_detections(gd, od, tol=1e-4):
+    bad = []
+    if [d.id for d in gd] != [d["id"] for d in od]:
+        return ["ids differ: %s vs %s" % ([d.id for d in gd], [d["id"] for d in od])]
+    for a, b in zip(gd, od):
+        if a.hamming != b["hamming"]:
+            bad.append("hamming id %d" % a.id)
+        if abs(a.decision_margin - b["decision_margin"]) > tol:
+            bad.append("margin id %d %r vs %r" % (a.id, a.decision_margin, b["decision_margin"]))
+        for nm, x, y in [("H", a.H, b["H"]), ("c", a.c, b["c"]), ("p", a.p, b["p"])]:
+            if not np.allclose(x, y, rtol=0, atol=tol):
+                bad.append("%s id %d max diff %g" % (nm, a.id, float(np.max(np.abs(x - y)))))
+            if not np.array_equal(np.floor(x), np.floor(y)) and nm != "H":
+                bad.append("integer %s id %d differ" % (nm, a.id))
+    return bad
