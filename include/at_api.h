@@ -131,6 +131,15 @@ typedef struct {
   float corners[4][2];     /* after AdjustPixelCenters (full resolution) */
 } at_quad_record;
 
+/* Per-stage GPU timing with HIP events between the kernels of the launch
+ * sequence (the reference times every stage with CudaEvents and logs them at
+ * VLOG(1), apriltag_gpu.cu:1118-1163).  at_stage_times writes the mean
+ * milliseconds per batch of each stage to ms[0..n-1] and the number of timed
+ * batches to ms[n]; returns n (the stage count) or < 0. */
+int at_set_profiling(at_detector *d, int enable);
+int at_stage_times(at_detector *d, double *ms, int cap);
+const char *at_stage_name(int stage);
+
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);
 

@@ -70,6 +70,8 @@ def lib():
         L.ao_family_code.restype = C.c_uint64
         L.ao_family_code.argtypes = [C.c_int]
         L.ao_family_ncodes.restype = C.c_int
+        L.ao_family_id.restype = C.c_int
+        L.ao_family_id.argtypes = [C.c_int]
         L.ao_family_bit.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         for n in ["ao_det_atan2f", "ao_det_hypotf"]:
             getattr(L, n).restype = C.c_float
@@ -180,6 +182,6 @@ class Oracle:
         return lib().ao_status(self.h)
 
 
-def family_codes():
+def family_entries():
     L = lib()
-    return [int(L.ao_family_code(i)) for i in range(L.ao_family_ncodes())]
+    return [(int(L.ao_family_id(i)), int(L.ao_family_code(i))) for i in range(L.ao_family_ncodes())]

@@ -21,7 +21,7 @@
 namespace at {
 hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st);
+                           hipStream_t st, hipEvent_t* ev);
 
 struct CodeEntry {
   int id;
@@ -57,6 +57,10 @@ struct at_detector {
   int last_nframes;
   int pending;
   hipEvent_t ev_done;
+  int profiling;
+  hipEvent_t ev_stage[kNumStages + 1];
+  double stage_ms[kNumStages];
+  long stage_batches;
 };
 
 static int hip_fail(hipError_t e) {
@@ -129,6 +133,8 @@ void at_destroy(at_detector* d) {
   if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
   if (d->h_dets) (void)hipHostFree(d->h_dets);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+  for (int i = 0; i <= kNumStages; i++)
+    if (d->ev_stage[i]) (void)hipEventDestroy(d->ev_stage[i]);
   if (d->st) (void)hipStreamDestroy(d->st);
   delete d;
 }
@@ -330,7 +336,7 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   hipStream_t st = d->st;
   HIPCHK(hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st));
-  HIPCHK(launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st));
+  HIPCHK(launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, d->profiling ? d->ev_stage : nullptr));
   HIPCHK(hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
                         hipMemcpyDeviceToHost, st));
@@ -344,6 +350,14 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   if (!d->pending) return AT_E_INVALID;
   HIPCHK(hipEventSynchronize(d->ev_done));
   d->pending = 0;
+  if (d->profiling) {
+    for (int i = 0; i < kNumStages; i++) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, d->ev_stage[i], d->ev_stage[i + 1]));
+      d->stage_ms[i] += ms;
+    }
+    d->stage_batches++;
+  }
   const int B = d->B;
   int rc = AT_OK;
   for (int f = 0; f < d->last_nframes; f++) {
@@ -412,6 +426,29 @@ int at_detect_device(at_detector* d, const void* d_frames, size_t frame_stride, 
   int rc = at_enqueue_device(d, d_frames, frame_stride, nframes, fmt);
   if (rc) return rc;
   return at_collect(d, out, cap_per_frame, n_per_frame);
+}
+
+int at_set_profiling(at_detector* d, int enable) {
+  if (!d) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));
+  if (enable && !d->ev_stage[0])
+    for (int i = 0; i <= kNumStages; i++) HIPCHK(hipEventCreate(&d->ev_stage[i]));
+  d->profiling = enable ? 1 : 0;
+  for (int i = 0; i < kNumStages; i++) d->stage_ms[i] = 0;
+  d->stage_batches = 0;
+  return AT_OK;
+}
+
+int at_stage_times(at_detector* d, double* ms, int cap) {
+  if (!d || !ms || cap < kNumStages + 1) return AT_E_INVALID;
+  for (int i = 0; i < kNumStages; i++) ms[i] = d->stage_batches ? d->stage_ms[i] / d->stage_batches : 0.0;
+  ms[kNumStages] = (double)d->stage_batches;
+  return kNumStages;
+}
+
+const char* at_stage_name(int stage) {
+  return (stage >= 0 && stage < kNumStages) ? kStageNames[stage] : "";
 }
 
 int at_frame_status(at_detector* d, int frame) {

@@ -13,10 +13,15 @@ constexpr int kHashSlots = 16384;      // per-frame open-addressing table of blo
 constexpr int kHashBits = 14;
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kMaxDets = 128;          // candidate detections per frame
-constexpr int kMaxQuads = 512;         // fitted-quad debug records per frame
+constexpr int kMaxQuads = 2048;        // fitted-quad debug records per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
 constexpr int kNMaxima = 10;
+
+// ---- stages of one launch sequence (per-stage event timing) ----------------
+constexpr int kNumStages = 8;
+constexpr const char* kStageNames[kNumStages] = {"k_pre", "k_thr_ccl", "k_ccl_border", "k_ccl_final",
+                                                 "k_boundary", "k_pairs", "k_group", "k_blob"};
 
 // ---- per-frame status bits -------------------------------------------------
 constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs

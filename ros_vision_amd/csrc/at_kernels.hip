@@ -1544,30 +1544,45 @@ hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_book), &cb, sizeof(cb));
 }
 
+// Kernel order of one launch sequence; ev (optional, kNumStages+1 events)
+// brackets every kernel for per-stage timing.
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st) {
+                           hipStream_t st, hipEvent_t* ev) {
+  int e = 0;
+  auto mark = [&]() {
+    if (ev) (void)hipEventRecord(ev[e++], st);
+  };
+  mark();
   {
     dim3 blk(64, 4), grd((g.TW + 63) / 64, (g.TH + 3) / 4, B);
     if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
     else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
     else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
   }
+  mark();
   {
     dim3 grd(g.CTX, g.CTY, B);
     hipLaunchKernelGGL(k_thr_ccl, grd, dim3(256), 0, st, b, g, prm);
+    mark();
     hipLaunchKernelGGL(k_ccl_border, grd, dim3(64), 0, st, b, g);
+    mark();
   }
   {
     dim3 blk(64, 4), grd((g.BW + 63) / 64, (g.BH + 3) / 4, B);
     hipLaunchKernelGGL(k_ccl_final, grd, blk, 0, st, b, g);
+    mark();
   }
   {
     dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 3) / 4, B);
     hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
+    mark();
   }
   hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g);
+  mark();
   hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
+  mark();
   hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
+  mark();
   return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ EXPORTS = [
     "at_config_default", "at_create", "at_detect", "at_detect_batch", "at_detect_device",
     "at_enqueue_device", "at_collect", "at_frame_status", "at_debug_copy", "at_destroy",
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
+    "at_set_profiling", "at_stage_times", "at_stage_name",
 ]
 
 
@@ -104,6 +105,14 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError("libat_hip.so not built: run `make -C ros_vision_amd/csrc` "
                            "(or __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7
+    # (same soname as /opt/rocm's).  Whichever loads first is the one both use,
+    # and torch only initialises on its own copy, so let torch load first when
+    # it is installed (it provides device memory / torch.distributed to callers).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     L.at_config_default.argtypes = [C.POINTER(AtConfig), C.c_int, C.c_int]
     L.at_create.argtypes = [C.POINTER(AtConfig), C.POINTER(AtCamera), C.POINTER(C.c_void_p)]
@@ -122,6 +131,10 @@ def load_library(path: str = LIB_PATH):
     L.at_strerror.argtypes = [C.c_int]
     L.at_family_num_known.argtypes = [C.c_char_p]
     L.at_family_entry.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+    L.at_set_profiling.argtypes = [C.c_void_p, C.c_int]
+    L.at_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
+    L.at_stage_name.restype = C.c_char_p
+    L.at_stage_name.argtypes = [C.c_int]
     _LIB = L
     return L
 
@@ -235,6 +248,19 @@ class GpuDetector:
             _check(rc, "at_collect")
         return self._unpack(self._pending)
 
+    # ---- per-stage timing (the reference's CudaEvent stage timers,
+    #      apriltag_gpu.cu:1118-1163) ----------------------------------------
+    def set_profiling(self, enable=True):
+        _check(load_library().at_set_profiling(self._h, int(enable)), "at_set_profiling")
+
+    def stage_times(self):
+        """{stage name: (mean ms per batch, batches)} accumulated since profiling was enabled."""
+        L = load_library()
+        buf = (C.c_double * 32)()
+        n = _check(L.at_stage_times(self._h, buf, 32), "at_stage_times")
+        batches = int(buf[n]) if n < 32 else 0
+        return {L.at_stage_name(i).decode(): buf[i] for i in range(n)}, batches
+
     def detections(self, frame=0):
         """GpuDetector::Detections (apriltag_gpu.h:93), sorted by id."""
         return self._last[frame]
@@ -285,7 +311,7 @@ class GpuDetector:
         return self._copy(AT_STAGE_BLOB_POINTS, frame, need, np.uint64)
 
     def copy_quads(self, frame=0):
-        recs = (AtQuadRecord * 512)()
+        recs = (AtQuadRecord * 2048)()
         n = load_library().at_debug_copy(self._h, AT_STAGE_QUADS, frame, C.cast(recs, C.c_void_p), C.sizeof(recs))
         _check(int(n), "at_debug_copy")
         out = []

@@ -10,7 +10,7 @@ from ros_vision_amd import synth
 
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 os.makedirs(out, exist_ok=True)
-cases = [("syn0", 1280, 720, synth.stream_frame(1280, 720, 0)[0], 0)]
+cases = [("syn1080", 1920, 1080, synth.to_yuyv(synth.render_board(1920, 1080, seed=4242, ntags=24)[0]), 0)]
 for name, W, H, frame, fmt in cases:
     det = rva.GpuDetector(W, H)
     dets = det.detect(frame, fmt)
@@ -20,5 +20,4 @@ for name, W, H, frame, fmt in cases:
                                          *q["corners"].ravel()) for q in det.copy_quads()], np.float64),
                         ids=np.array([d.id for d in dets]), npairs=det.num_pairs())
     print(name, "dets", [d.id for d in dets], "pairs", det.num_pairs())
-import torch
-print("torch", torch.__version__, torch.cuda.is_available(), torch.cuda.device_count())
+
