@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- frames/s and p50 per-frame latency of 1280x720 AprilTag detection
+on N MI355X (BASELINE.json metric; workload = configs[1], a single-camera
+1280x720 tag36h11 synthetic stream).
+
+A *step* is one launch sequence over a batch of B frames that are already
+resident in HBM (see DESIGN.md "Measurement").  Each rank owns its own shard of
+the stream (weak scaling, no data-path collective: frames are independent).
+Two detector instances on two HIP streams are used round-robin so the host
+tail (reconcile + sort by id) of batch k overlaps the kernels of batch k+1.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  Latency: frames fed one at a time (B = 1) from
+HBM to detections in host memory.  cpu_baseline: the C oracle
+(oracle/ao_bench, restatement of the reference pipeline) on host cores.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec + p50 per-frame latency, 1280x720 AprilTag detect at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
+    ap.add_argument("--pool", type=int, default=64, help="distinct synthetic frames per GPU")
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--tags", type=int, default=15)
+    ap.add_argument("--latency-frames", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-profile", action="store_true")
+    return ap.parse_args()
+
+
+def render_pool(args, rank):
+    from ros_vision_amd import synth
+    codes = dict(__import__("ros_vision_amd").family_entries())
+    frames = np.empty((args.pool, args.height, 2 * args.width), np.uint8)
+    for i in range(args.pool):
+        gray, _ = synth.render_board(args.width, args.height, seed=766000 + rank * args.pool + i,
+                                     ntags=args.tags, codes=codes)
+        frames[i] = synth.to_yuyv(gray)
+    return frames
+
+
+def cpu_baseline(frames, width, height):
+    """Time the C oracle on this host (rank 0, N=1 only): ~10-20 s of CPU work."""
+    exe = os.path.join(ROOT, "oracle", "ao_bench")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-s"], check=True)
+    cores = min(16, len(os.sched_getaffinity(0)))
+    nf = min(16, frames.shape[0])
+    with tempfile.NamedTemporaryFile(suffix=".raw", delete=False) as f:
+        frames[:nf].tofile(f)
+        path = f.name
+    try:
+        lat_iters, thr_iters = 100, 30
+        out = subprocess.run([exe, path, str(width), str(height), str(nf), str(lat_iters), str(thr_iters),
+                              str(cores)], check=True, capture_output=True, text=True, timeout=600).stdout
+    finally:
+        os.unlink(path)
+    r = json.loads(out.strip().splitlines()[-1])
+    return {"value": round(r["throughput_fps"], 3), "unit": "frames/s", "cores": r["threads"],
+            "kind": "port", "p50_ms_1thread": round(r["p50_ms"], 3),
+            "sample": "C oracle (restatement of the reference pipeline incl. decode), %d distinct 1280x720 "
+                      "synthetic frames: %d frames single-thread for latency, %d threads x %d frames for "
+                      "throughput" % (nf, lat_iters, r["threads"], thr_iters)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # device memory + torch.distributed; loads the HIP runtime first
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+
+    import ros_vision_amd as rva
+    W, H, B = args.width, args.height, args.batch
+    assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
+    frames = render_pool(args, rank)
+    d_frames = torch.from_numpy(frames).to("cuda")
+    stride = frames[0].nbytes
+    base = d_frames.data_ptr()
+    npool = args.pool
+    dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank) for _ in range(2)]
+
+    def batch_ptr(step):
+        off = (step * B) % npool
+        if off + B > npool:
+            off = 0
+        return base + off * stride
+
+    def run(nsteps, step0=0):
+        """Round-robin over two detectors: enqueue k, then collect k-1."""
+        ndet = 0
+        prev = None
+        for s in range(nsteps):
+            d = dets[s % 2]
+            d.enqueue_device(batch_ptr(step0 + s), stride, B)
+            if prev is not None:
+                ndet += sum(len(x) for x in prev.collect())
+            prev = d
+        if prev is not None:
+            ndet += sum(len(x) for x in prev.collect())
+        return ndet
+
+    run(max(1, args.warmup))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ndet = run(args.steps, step0=args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nd = torch.tensor([ndet], dtype=torch.float64, device="cuda")
+        dist.all_reduce(nd, op=dist.ReduceOp.SUM)
+        ndet = int(nd.item())
+    total_frames = world * args.steps * B
+    fps = total_frames / elapsed
+
+    # per-frame latency: one frame at a time, HBM -> detections in host memory
+    lat_det = rva.GpuDetector(W, H, max_batch=1, device=local_rank)
+    for i in range(10):
+        lat_det.detect_device(base + (i % npool) * stride, stride, 1)
+    lat = []
+    for i in range(args.latency_frames):
+        t1 = time.perf_counter()
+        lat_det.detect_device(base + (i % npool) * stride, stride, 1)
+        lat.append(time.perf_counter() - t1)
+    lat = np.array(lat) * 1e3
+
+    # per-stage GPU time (HIP events on the detector's stream), separate pass
+    stages, stage_batches = {}, 0
+    if not args.no_stage_profile:
+        prof = dets[0]
+        prof.set_profiling(True)
+        for s in range(10):
+            prof.enqueue_device(batch_ptr(s), stride, B)
+            prof.collect()
+        stages, stage_batches = prof.stage_times()
+        prof.set_profiling(False)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    algo_bytes_per_frame = 3 * W * H  # read YUYV 2WH + write gray WH
+    per_gpu_fps = fps / world
+    achieved = per_gpu_fps * algo_bytes_per_frame / 1e9
+    pipe_ms = sum(stages.values()) if stages else None
+    dominant = max(stages, key=stages.get) if stages else None
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("width") == W and tj.get("height") == H:
+                traffic = tj.get("hbm_bytes_per_frame")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": round(fps, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": "configs[1]: 1280x720 single-camera synthetic tag36h11 stream "
+                               "(%d tags/frame, YUYV, frames resident in HBM)" % args.tags,
+                   "width": W, "height": H, "batch_per_gpu": B, "distinct_frames_per_gpu": npool,
+                   "parallelism": "frame-sharded x%d (no data-path collective)" % world},
+        "p50_latency_ms": round(float(np.percentile(lat, 50)), 4),
+        "p99_latency_ms": round(float(np.percentile(lat, 99)), 4),
+        "detections_per_frame": round(ndet / total_frames, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "bytes_per_frame": algo_bytes_per_frame,
+                     "note": "achieved = per-GPU frames/s x algorithmic bytes 3*W*H (BASELINE.md)"},
+        "stage_ms_per_batch": {k: round(v, 4) for k, v in stages.items()},
+        "dominant_kernel": dominant,
+        "pipeline_gpu_ms_per_batch": round(pipe_ms, 4) if pipe_ms else None,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(frames, W, H)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": str(e)[:200]}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
