@@ -174,6 +174,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.refine_edges = cfg->refine_edges;
   p.fx = cam->fx; p.fy = cam->fy; p.cx = cam->cx; p.cy = cam->cy;
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
+  p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
 
   auto fail = [&](int code) {
     at_destroy(d);
@@ -223,7 +224,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.work = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
   b.quads = (QuadRecord*)dalloc(B * kMaxQuads * sizeof(QuadRecord));
-  d->ctrl_words = 5 * B + 2;
+  d->ctrl_words = 5 * B + 4;
   d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
   b.npts = d->d_ctrl;
   b.npairs = d->d_ctrl + B;
@@ -232,6 +233,10 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.status = d->d_ctrl + 4 * B;
   b.nwork = d->d_ctrl + 5 * B;
   b.workhead = d->d_ctrl + 5 * B + 1;
+  b.nqcand = d->d_ctrl + 5 * B + 2;
+  b.qhead = d->d_ctrl + 5 * B + 3;
+  b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
+  b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   const size_t nw = (size_t)d->nblobwg;
   b.s_i32 = (int32_t*)dalloc(nw * 3 * kSortCap * 4);
   b.s_i64 = (int64_t*)dalloc(nw * 3 * kSortCap * 8);
@@ -364,7 +369,7 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
     const uint32_t status = d->h_ctrl[4 * B + f];
     const int ncand = (int)std::min<uint32_t>(d->h_ctrl[2 * B + f], (uint32_t)kMaxDets);
     int n = 0;
-    if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow)) {
+    if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow)) {
       rc = AT_E_CAPACITY;
     } else {
       n = host_tail(d->h_dets + (size_t)f * kMaxDets, ncand, out ? out + (size_t)f * cap_per_frame : nullptr,
@@ -454,7 +459,9 @@ const char* at_stage_name(int stage) {
 int at_frame_status(at_detector* d, int frame) {
   if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
   const uint32_t s = d->h_ctrl[4 * d->B + frame];
-  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow)) ? AT_E_CAPACITY : AT_OK;
+  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow))
+             ? AT_E_CAPACITY
+             : AT_OK;
 }
 
 long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t bytes) {

@@ -19,15 +19,17 @@ constexpr int kBlobThreads = 256;
 constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
-constexpr int kNumStages = 8;
-constexpr const char* kStageNames[kNumStages] = {"k_pre", "k_thr_ccl", "k_ccl_border", "k_ccl_final",
-                                                 "k_boundary", "k_pairs", "k_group", "k_blob"};
+constexpr int kNumStages = 9;
+constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final", "k_boundary",
+                                                 "k_pairs", "k_group",   "k_blob",       "k_decode"};
 
 // ---- per-frame status bits -------------------------------------------------
 constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs
 constexpr uint32_t kStatusHashFull = 2u;
 constexpr uint32_t kStatusDetsOverflow = 4u;
 constexpr uint32_t kStatusPointsOverflow = 8u;
+constexpr uint32_t kStatusQuadsOverflow = 16u;
+constexpr int kQuadCandPerFrame = 512;  // accepted quads queued for decode, per frame of the batch
 
 // Frame geometry (all derived from W, H).
 struct Geom {
@@ -48,6 +50,7 @@ struct Params {
   double decode_sharpening;
   int refine_edges;
   double fx, fy, cx, cy, k1, k2, p1, p2, k3;
+  int diag_stop;  // diagnostics only (AT_DIAG_BLOB_STOP): k_blob returns after phase N; 0 = full
 };
 
 // One detection candidate as produced on the device (before reconcile).
@@ -58,6 +61,12 @@ struct DevDetection {
   double H[9];
   double c[2];
   double p[4][2];
+};
+
+// Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode.
+struct QuadCand {
+  uint32_t frame, rank;
+  float p[4][2];
 };
 
 struct QuadRecord {
@@ -97,6 +106,10 @@ struct DevBufs {
   uint32_t* status;   // [B]
   uint32_t* nwork;    // [1]
   uint32_t* workhead; // [1]
+  uint32_t* nqcand;   // [1]
+  uint32_t* qhead;    // [1]
+  QuadCand* qcand;    // [qcand_cap]
+  uint32_t qcand_cap;
   // per-workgroup scratch of the blob kernel
   int32_t* s_i32;     // [nblobwg][3][kSortCap]  prefix Mx, My, W
   int64_t* s_i64;     // [nblobwg][3][kSortCap]  prefix Mxx, Myy, Mxy

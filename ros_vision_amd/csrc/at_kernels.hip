@@ -488,8 +488,43 @@ __device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
   return 1 + (uint32_t)__builtin_ctzll(rest);
 }
 
+constexpr int kLdsPairSlots = 512;
+
+__device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uint64_t key, uint32_t len) {
+  uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
+  for (int probe = 0; probe < kLdsPairSlots; probe++) {
+    const uint64_t k = keys[h];
+    if (k == key) {
+      atomicAdd(cnts + h, len);
+      return true;
+    }
+    if (k == 0) {
+      const uint64_t prev = atomicCAS((unsigned long long*)(keys + h), 0ull, (unsigned long long)key);
+      if (prev == 0 || prev == key) {
+        atomicAdd(cnts + h, len);
+        return true;
+      }
+    }
+    h = (h + 1) & (kLdsPairSlots - 1);
+  }
+  return false;
+}
+
+// One 256-thread workgroup covers 64x4 interior pixels (up to 1024 points).
+// Points are compacted with a block scan and ONE global atomic per workgroup;
+// the pair histogram is aggregated in an LDS hash table (lane runs first) and
+// flushed with one global atomic per distinct pair per workgroup.
 __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
+  __shared__ uint64_t s_pkey[kLdsPairSlots];
+  __shared__ uint32_t s_pcnt[kLdsPairSlots];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_base;
   const int f = blockIdx.z;
+  const int tid = threadIdx.y * 64 + threadIdx.x;
+  for (int i = tid; i < kLdsPairSlots; i += 256) {
+    s_pkey[i] = 0;
+    s_pcnt[i] = 0;
+  }
   const int x = 1 + blockIdx.x * 64 + threadIdx.x;
   const int y = 1 + blockIdx.y * 4 + threadIdx.y;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
@@ -514,33 +549,60 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       if (!dedup && v0 + vdl == 255 && size[ldl] >= 25) pk[3] = make_qbp(rep0, ldl, x, y, 3, vdl > v0);
     }
   }
+  __syncthreads();  // LDS table initialised
   const uint32_t lane = lane_id();
-  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
   uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
   uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
+  uint32_t npk = 0;
 #pragma unroll
   for (int dir = 0; dir < 4; dir++) {
     const bool has = pk[dir] != 0;
-    const uint64_t m = __ballot(has);
-    if (m == 0) continue;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(b.npts + f, (uint32_t)__popcll(m));
-    base = __shfl(base, 0);
-    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-    if (has) {
-      if (pos < (uint32_t)g.cap_pts) pts[pos] = pk[dir];
-      else atomicOr(b.status + f, kStatusPointsOverflow);
-    }
-    // pair histogram, aggregated over runs of equal pairs
+    npk += has;
     const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
     const uint64_t prev = __shfl_up(r01, 1);
     const bool same = has && lane > 0 && prev == r01;
     const uint64_t same_mask = __ballot(same);
     if (has && !same) {
       const uint32_t len = run_len(same_mask, lane);
-      const uint32_t s = ht_slot_insert(ht_key, r01);
+      if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) {
+        const uint32_t s = ht_slot_insert(ht_key, r01);
+        if (s == 0xffffffffu) atomicOr(b.status + f, kStatusHashFull);
+        else atomicAdd(ht_cnt + s, len);
+      }
+    }
+  }
+  // block-wide exclusive scan of the per-thread point counts
+  uint32_t incl = npk;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  const int w = tid >> 6;
+  if (lane == 63) s_wsum[w] = incl;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int i = 0; i < w; i++) wbase += s_wsum[i];
+  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  if (tid == 0) s_base = total ? atomicAdd(b.npts + f, total) : 0u;
+  __syncthreads();
+  uint32_t pos = s_base + wbase + incl - npk;
+  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
+#pragma unroll
+  for (int dir = 0; dir < 4; dir++) {
+    if (pk[dir]) {
+      if (pos < (uint32_t)g.cap_pts) pts[pos] = pk[dir];
+      else atomicOr(b.status + f, kStatusPointsOverflow);
+      pos++;
+    }
+  }
+  // flush the workgroup's pair histogram
+  for (int i = tid; i < kLdsPairSlots; i += 256) {
+    const uint64_t k = s_pkey[i];
+    if (k) {
+      const uint32_t s = ht_slot_insert(ht_key, k);
       if (s == 0xffffffffu) atomicOr(b.status + f, kStatusHashFull);
-      else atomicAdd(ht_cnt + s, len);
+      else atomicAdd(ht_cnt + s, s_pcnt[i]);
     }
   }
 }
@@ -920,46 +982,45 @@ __device__ __forceinline__ uint64_t rotate90_36(uint64_t w) {
   return ((w << 9) | (w >> 27)) & ((1ull << 36) - 1);
 }
 
-__device__ __forceinline__ void unrank(int t, int* m) {
-  int c = 0;
-  for (int a = 0; a < 10; a++)
-    for (int bq = a + 1; bq < 10; bq++)
-      for (int d = bq + 1; d < 10; d++)
-        for (int e = d + 1; e < 10; e++) {
-          if (c == t) { m[0] = a; m[1] = bq; m[2] = d; m[3] = e; return; }
-          c++;
-        }
+// lexicographic 4-combinations of 10 maxima == Unrank (line_fit_filter.cu:709-728)
+__constant__ uint8_t c_combo[210][4] = {{0,1,2,3},{0,1,2,4},{0,1,2,5},{0,1,2,6},{0,1,2,7},{0,1,2,8},{0,1,2,9},{0,1,3,4},{0,1,3,5},{0,1,3,6},{0,1,3,7},{0,1,3,8},{0,1,3,9},{0,1,4,5},{0,1,4,6},{0,1,4,7},{0,1,4,8},{0,1,4,9},{0,1,5,6},{0,1,5,7},{0,1,5,8},{0,1,5,9},{0,1,6,7},{0,1,6,8},{0,1,6,9},{0,1,7,8},{0,1,7,9},{0,1,8,9},{0,2,3,4},{0,2,3,5},{0,2,3,6},{0,2,3,7},{0,2,3,8},{0,2,3,9},{0,2,4,5},{0,2,4,6},{0,2,4,7},{0,2,4,8},{0,2,4,9},{0,2,5,6},{0,2,5,7},{0,2,5,8},{0,2,5,9},{0,2,6,7},{0,2,6,8},{0,2,6,9},{0,2,7,8},{0,2,7,9},{0,2,8,9},{0,3,4,5},{0,3,4,6},{0,3,4,7},{0,3,4,8},{0,3,4,9},{0,3,5,6},{0,3,5,7},{0,3,5,8},{0,3,5,9},{0,3,6,7},{0,3,6,8},{0,3,6,9},{0,3,7,8},{0,3,7,9},{0,3,8,9},{0,4,5,6},{0,4,5,7},{0,4,5,8},{0,4,5,9},{0,4,6,7},{0,4,6,8},{0,4,6,9},{0,4,7,8},{0,4,7,9},{0,4,8,9},{0,5,6,7},{0,5,6,8},{0,5,6,9},{0,5,7,8},{0,5,7,9},{0,5,8,9},{0,6,7,8},{0,6,7,9},{0,6,8,9},{0,7,8,9},{1,2,3,4},{1,2,3,5},{1,2,3,6},{1,2,3,7},{1,2,3,8},{1,2,3,9},{1,2,4,5},{1,2,4,6},{1,2,4,7},{1,2,4,8},{1,2,4,9},{1,2,5,6},{1,2,5,7},{1,2,5,8},{1,2,5,9},{1,2,6,7},{1,2,6,8},{1,2,6,9},{1,2,7,8},{1,2,7,9},{1,2,8,9},{1,3,4,5},{1,3,4,6},{1,3,4,7},{1,3,4,8},{1,3,4,9},{1,3,5,6},{1,3,5,7},{1,3,5,8},{1,3,5,9},{1,3,6,7},{1,3,6,8},{1,3,6,9},{1,3,7,8},{1,3,7,9},{1,3,8,9},{1,4,5,6},{1,4,5,7},{1,4,5,8},{1,4,5,9},{1,4,6,7},{1,4,6,8},{1,4,6,9},{1,4,7,8},{1,4,7,9},{1,4,8,9},{1,5,6,7},{1,5,6,8},{1,5,6,9},{1,5,7,8},{1,5,7,9},{1,5,8,9},{1,6,7,8},{1,6,7,9},{1,6,8,9},{1,7,8,9},{2,3,4,5},{2,3,4,6},{2,3,4,7},{2,3,4,8},{2,3,4,9},{2,3,5,6},{2,3,5,7},{2,3,5,8},{2,3,5,9},{2,3,6,7},{2,3,6,8},{2,3,6,9},{2,3,7,8},{2,3,7,9},{2,3,8,9},{2,4,5,6},{2,4,5,7},{2,4,5,8},{2,4,5,9},{2,4,6,7},{2,4,6,8},{2,4,6,9},{2,4,7,8},{2,4,7,9},{2,4,8,9},{2,5,6,7},{2,5,6,8},{2,5,6,9},{2,5,7,8},{2,5,7,9},{2,5,8,9},{2,6,7,8},{2,6,7,9},{2,6,8,9},{2,7,8,9},{3,4,5,6},{3,4,5,7},{3,4,5,8},{3,4,5,9},{3,4,6,7},{3,4,6,8},{3,4,6,9},{3,4,7,8},{3,4,7,9},{3,4,8,9},{3,5,6,7},{3,5,6,8},{3,5,6,9},{3,5,7,8},{3,5,7,9},{3,5,8,9},{3,6,7,8},{3,6,7,9},{3,6,8,9},{3,7,8,9},{4,5,6,7},{4,5,6,8},{4,5,6,9},{4,5,7,8},{4,5,7,9},{4,5,8,9},{4,6,7,8},{4,6,7,9},{4,6,8,9},{4,7,8,9},{5,6,7,8},{5,6,7,9},{5,6,8,9},{5,7,8,9},{6,7,8,9}};
+// (m0, m1) pairs of Compute{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7}Fit / Get{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7} (line_fit_filter.cu:731-743, 936-972)
+__constant__ uint8_t c_m0m1[28][2] = {{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7}};
+
+struct LineFitOut {
+  double err, mse;
+  double p01[2], p23[2];
+};
+
+// FitLine by value (no pointers -> no scratch traffic)
+template <bool kP01, bool kP23>
+__device__ __forceinline__ LineFitOut fit_line_v(const Moments& m) {
+  LineFitOut o;
+  fit_line(m, kP01 ? o.p01 : nullptr, kP23 ? o.p23 : nullptr, &o.err, &o.mse);
+  return o;
 }
 
 struct BlobShared {
-  union {
-    uint64_t keys[kSortCap];                 // point sort keys, later peak keys
-    struct { double sx[kSortCap / 2]; double sy[kSortCap / 2]; } smp;  // refine samples
-  } u;
+  uint64_t keys[kSortCap];  // point sort keys, later peak keys
   double red_f64[4];
   int64_t red_i64[4];
   uint32_t red_u32[4];
   int32_t red_i32[4];
-  uint64_t red_u64[4];
-  uint32_t item, nwork, npeaks, best_code;
+  uint32_t red_idx[4];
+  uint32_t item, nwork, npeaks;
   int32_t pi[16];
   double e01[7][7];
   double lp01[7][7][2];
-  double combo_err[210];
-  int ok;
-  float qc[4][2];
-  int nsamp[4], samp_off[4];
-  float enx[4], eny[4];
   double lines[4][4];
-  double H[9];
-  double gmx[64], gmy[64], gmv[64];
-  int gmvalid[64];
-  double values[100];
 };
 
+// K9a: one blob pair per workgroup iteration (persistent, work-list driven):
+// extents + SelectBlobs, theta sort, line-fit prefix sums, errors, filter,
+// peaks, FitQuads, UpdateFitQuads.  Accepted quads go to the decode list.
 __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared S;
   const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
   BlobScratch P;
   {
     const size_t wg = blockIdx.x;
@@ -988,7 +1049,6 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
     uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
     const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
-    const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
 
     // ---- extents (P3) ---------------------------------------------------------
     uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
@@ -996,7 +1056,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     int64_t spg = 0;
     for (uint32_t t = tid; t < n; t += kBlobThreads) {
       const uint64_t k = grp[t];
-      S.u.keys[t] = k;
+      S.keys[t] = k;
       const int dxy = (int)(k & 3);
       const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
       const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
@@ -1019,13 +1079,14 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
     keep = keep && !((double)ext_dot(e) < 0.0);
     if (!keep) continue;  // uniform across the workgroup
+    if (prm.diag_stop == 1) continue;
     if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
     const uint32_t bi = rank & 0xfff;
 
-    // ---- theta + sort key (P5/P6): (theta, dxy, y, x) -------------------------
+    // ---- theta + sort key (P5/P6): (theta, plane, y, x) -----------------------
     const double cx = ext_cx(e), cy = ext_cy(e);
     for (uint32_t t = tid; t < n; t += kBlobThreads) {
-      const uint64_t k = S.u.keys[t];
+      const uint64_t k = S.keys[t];
       const int dxy = (int)(k & 3);
       const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
       const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
@@ -1035,14 +1096,15 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       long long ti = (long long)rintf(theta);
       if (ti < 0) ti = 0;
       // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
-      S.u.keys[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
-                    ((uint64_t)bx << 1) | ((k >> 3) & 1);
+      S.keys[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
+                  ((uint64_t)bx << 1) | ((k >> 3) & 1);
     }
     int np2 = 64;
     while (np2 < (int)n) np2 <<= 1;
-    for (int t = (int)n + tid; t < np2; t += kBlobThreads) S.u.keys[t] = ~0ull;
+    for (int t = (int)n + tid; t < np2; t += kBlobThreads) S.keys[t] = ~0ull;
     __syncthreads();
-    block_bitonic_sort<uint64_t, kBlobThreads>(S.u.keys, np2);
+    block_bitonic_sort<uint64_t, kBlobThreads>(S.keys, np2);
+    if (prm.diag_stop == 2) continue;
 
     // ---- line-fit points + per-blob inclusive prefix sums (P7) -----------------
     {
@@ -1054,7 +1116,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         uint32_t vMx = 0, vMy = 0, vW = 0;
         int64_t vMxx = 0, vMyy = 0, vMxy = 0;
         if (t < n) {
-          const uint64_t sk = S.u.keys[t];
+          const uint64_t sk = S.keys[t];
           const int dxy = (int)((sk >> 21) & 3);
           const int32_t ix2 = (int32_t)(((sk >> 1) & 0x3ff) * 2 + dx_of(dxy)) + 1;
           const int32_t iy2 = (int32_t)(((sk >> 11) & 0x3ff) * 2 + dy_of(dxy)) + 1;
@@ -1073,14 +1135,14 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         const uint32_t pMx = block_incl_scan(vMx, S.red_u32, &tot) + cMx; cMx += tot;
         const uint32_t pMy = block_incl_scan(vMy, S.red_u32, &tot) + cMy; cMy += tot;
         const uint32_t pW = block_incl_scan(vW, S.red_u32, &tot) + cW; cW += tot;
-        int64_t pMxx = block_incl_scan(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
-        int64_t pMyy = block_incl_scan(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
-        int64_t pMxy = block_incl_scan(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
+        const int64_t pMxx = block_incl_scan(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
+        const int64_t pMyy = block_incl_scan(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
+        const int64_t pMxy = block_incl_scan(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
         if (t < n) {
           P.Mx[t] = (int32_t)pMx; P.My[t] = (int32_t)pMy; P.W[t] = (int32_t)pW;
           P.Mxx[t] = pMxx; P.Myy[t] = pMyy; P.Mxy[t] = pMxy;
-          // debug tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
-          const uint64_t sk = S.u.keys[t];
+          // parity tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
+          const uint64_t sk = S.keys[t];
           const uint64_t pbits = (((sk >> 1) & 0x3ff) << 14) | (((sk >> 11) & 0x3ff) << 4) | ((sk & 1) << 3) |
                                  ((sk >> 21) & 3);
           grp[t] = ((uint64_t)bi << 52) | (((sk >> 23) & 0xfffffff) << 24) | pbits;
@@ -1088,6 +1150,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       }
     }
     __syncthreads();
+    if (prm.diag_stop == 3) continue;
     // ---- errors, filter, peaks (K10 restated per blob, cyclic) ----------------
     const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
     for (uint32_t t = tid; t < n; t += kBlobThreads) {
@@ -1121,7 +1184,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         uint32_t u = __float_as_uint(ef);
         u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // cub radix float order
         const uint32_t slot = atomicAdd(&S.npeaks, 1u);
-        S.u.keys[slot] = ((uint64_t)u << 32) | t;
+        S.keys[slot] = ((uint64_t)u << 32) | t;
       }
     }
     __syncthreads();
@@ -1129,151 +1192,193 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     {
       int p2 = 2;
       while (p2 < (int)npk) p2 <<= 1;
-      for (int t = (int)npk + tid; t < p2; t += kBlobThreads) S.u.keys[t] = ~0ull;
+      for (int t = (int)npk + tid; t < p2; t += kBlobThreads) S.keys[t] = ~0ull;
       __syncthreads();
-      if (npk > 1) block_bitonic_sort<uint64_t, kBlobThreads>(S.u.keys, p2);
+      if (npk > 1) block_bitonic_sort<uint64_t, kBlobThreads>(S.keys, p2);
     }
+    if (prm.diag_stop == 4) continue;
     // ---- FitQuads (K11) --------------------------------------------------------
     const int cnt = (int)npk;
-    if (tid == 0) {
-      int pi[16];
-      for (int t = 0; t < 16; t++)
-        pi[t] = (t < cnt && t < kNMaxima) ? (int)(S.u.keys[t] & 0xffffffffu) : 0xffff;
-      for (int a2 = 1; a2 < 16; a2++) {
-        const int v = pi[a2];
-        int c2 = a2 - 1;
-        while (c2 >= 0 && pi[c2] > v) { pi[c2 + 1] = pi[c2]; c2--; }
-        pi[c2 + 1] = v;
+    if (tid < 16) {
+      // top min(10, cnt) peaks, re-sorted by point index (WarpMergeSort), pad 0xffff
+      const int v = (tid < cnt && tid < kNMaxima) ? (int)(S.keys[tid] & 0xffffffffu) : 0xffff;
+      int r = 0;
+      for (int j = 0; j < 16; j++) {
+        const int u = (j < cnt && j < kNMaxima) ? (int)(S.keys[j] & 0xffffffffu) : 0xffff;
+        r += (u < v) || (u == v && j < tid);
       }
-      for (int t = 0; t < 16; t++) S.pi[t] = pi[t];
+      S.pi[r] = v;
     }
     __syncthreads();
-    if (tid < 28) {
-      int m0 = 0, m1 = 0, c2 = 0;
-      for (int a2 = 0; a2 < 7; a2++)
-        for (int b2 = a2 + 1; b2 < 8; b2++) {
-          if (c2 == tid) { m0 = a2; m1 = b2; }
-          c2++;
-        }
-      if (cnt >= 4) {
-        if (m1 < kNMaxima && m1 < cnt) {
-          double err, mse;
-          fit_line(read_moments(P, n, S.pi[m0], S.pi[m1]), nullptr, S.lp01[m0][m1 - 1], &err, &mse);
-          if (mse > (double)prm.max_line_fit_mse) err = DBL_MAX;
-          S.e01[m0][m1 - 1] = err;
-        } else {
-          S.e01[m0][m1 - 1] = DBL_MAX;
-        }
+    if (cnt >= 4 && tid < 28) {
+      const int m0 = c_m0m1[tid][0], m1 = c_m0m1[tid][1];
+      if (m1 < kNMaxima && m1 < cnt) {
+        const LineFitOut o = fit_line_v<false, true>(read_moments(P, n, S.pi[m0], S.pi[m1]));
+        S.e01[m0][m1 - 1] = o.mse > (double)prm.max_line_fit_mse ? DBL_MAX : o.err;
+        S.lp01[m0][m1 - 1][0] = o.p23[0];
+        S.lp01[m0][m1 - 1][1] = o.p23[1];
+      } else {
+        S.e01[m0][m1 - 1] = DBL_MAX;
       }
     }
     __syncthreads();
-    if (tid < 210) {
-      int m[4];
-      unrank(tid, m);
-      double err = DBL_MAX;
-      if (cnt >= 4 && m[3] < kNMaxima && m[3] < cnt && S.e01[m[0]][m[1] - 1] != DBL_MAX) {
-        double e12, mse12, p12[2];
-        fit_line(read_moments(P, n, S.pi[m[1]], S.pi[m[2]]), nullptr, p12, &e12, &mse12);
-        if (!(mse12 > (double)prm.max_line_fit_mse)) {
-          const double* p01 = S.lp01[m[0]][m[1] - 1];
-          const double dot = p01[0] * p12[0] + p01[1] * p12[1];
+    if (prm.diag_stop == 7) continue;
+    double err = DBL_MAX;
+    if (tid < 210 && cnt >= 4) {
+      const int m0 = c_combo[tid][0], m1 = c_combo[tid][1], m2 = c_combo[tid][2], m3 = c_combo[tid][3];
+      const double e01 = S.e01[m0][m1 - 1];
+      if (m3 < cnt && e01 != DBL_MAX) {
+        const LineFitOut o12 = fit_line_v<false, true>(read_moments(P, n, S.pi[m1], S.pi[m2]));
+        if (!(o12.mse > (double)prm.max_line_fit_mse)) {
+          const double dot = S.lp01[m0][m1 - 1][0] * o12.p23[0] + S.lp01[m0][m1 - 1][1] * o12.p23[1];
           if (!(fabs(dot) > prm.cos_critical_rad)) {
-            double e23, mse23, e30, mse30;
-            fit_line(read_moments(P, n, S.pi[m[2]], S.pi[m[3]]), nullptr, nullptr, &e23, &mse23);
-            if (!(mse23 > (double)prm.max_line_fit_mse)) {
-              fit_line(read_moments(P, n, S.pi[m[3]], S.pi[m[0]]), nullptr, nullptr, &e30, &mse30);
-              if (!(mse30 > (double)prm.max_line_fit_mse)) err = S.e01[m[0]][m[1] - 1] + e12 + e23 + e30;
+            const LineFitOut o23 = fit_line_v<false, false>(read_moments(P, n, S.pi[m2], S.pi[m3]));
+            if (!(o23.mse > (double)prm.max_line_fit_mse)) {
+              const LineFitOut o30 = fit_line_v<false, false>(read_moments(P, n, S.pi[m3], S.pi[m0]));
+              if (!(o30.mse > (double)prm.max_line_fit_mse)) err = e01 + o12.err + o23.err + o30.err;
             }
           }
         }
       }
-      S.combo_err[tid] = err;
+    }
+    // BlockReduce(MinQuadError): minimum error, first (lowest) combination on ties
+    {
+      uint32_t bt = tid < 210 ? (uint32_t)tid : 0xffffffffu;
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) {
+        const double oe = __shfl_xor(err, d);
+        const uint32_t ot = __shfl_xor(bt, d);
+        if (oe < err || (oe == err && ot < bt)) { err = oe; bt = ot; }
+      }
+      if (lane == 0) { S.red_f64[tid >> 6] = err; S.red_idx[tid >> 6] = bt; }
+    }
+    __syncthreads();
+    if (prm.diag_stop == 8) continue;
+    double best = S.red_f64[0];
+    uint32_t bt = S.red_idx[0];
+    for (int i = 1; i < kBlobThreads / 64; i++)
+      if (S.red_f64[i] < best || (S.red_f64[i] == best && S.red_idx[i] < bt)) { best = S.red_f64[i]; bt = S.red_idx[i]; }
+    if (bt >= 210) bt = 0;
+    const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
+    uint16_t qidx[4];
+    for (int k = 0; k < 4; k++) qidx[k] = (uint16_t)S.pi[c_combo[bt][k]];
+    // UpdateFitQuads (apriltag_detect.cu:98-241): side lines in parallel, rest on one lane
+    if (valid && tid < 4) {
+      const LineFitOut o = fit_line_v<true, true>(read_moments(P, n, qidx[tid], qidx[(tid + 1) & 3]));
+      S.lines[tid][0] = o.p01[0];
+      S.lines[tid][1] = o.p01[1];
+      S.lines[tid][2] = o.p23[0];
+      S.lines[tid][3] = o.p23[1];
     }
     __syncthreads();
     if (tid == 0) {
-      int bt = 0;
-      double best = S.combo_err[0];
-      for (int t = 1; t < 210; t++)
-        if (S.combo_err[t] < best) { best = S.combo_err[t]; bt = t; }
-      int m[4];
-      unrank(bt, m);
-      const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
       QuadRecord rec;
       rec.blob_index = bi;
       rec.valid = valid;
-      rec.accepted = 0;
-      for (int k = 0; k < 4; k++) rec.indices[k] = (uint16_t)S.pi[m[k]];
-      int ok = 0;
-      if (valid) {
-        // UpdateFitQuads (apriltag_detect.cu:98-241)
-        double lines[4][4];
-        for (int k = 0; k < 4; k++) {
-          double err, mse;
-          fit_line(read_moments(P, n, rec.indices[k], rec.indices[(k + 1) & 3]), lines[k], lines[k] + 2, &err, &mse);
+      for (int k = 0; k < 4; k++) rec.indices[k] = qidx[k];
+      float qc[4][2];
+      int ok = valid;
+      for (int k = 0; ok && k < 4; k++) {
+        const int k1 = (k + 1) & 3;
+        const double A00 = S.lines[k][3], A01 = -S.lines[k1][3];
+        const double A10 = -S.lines[k][2], A11 = S.lines[k1][2];
+        const double B0 = -S.lines[k][0] + S.lines[k1][0];
+        const double B1 = -S.lines[k][1] + S.lines[k1][1];
+        const double det = A00 * A11 - A10 * A01;
+        const double W00 = A11 / det, W01 = -A01 / det;
+        if (fabs(det) < 0.001) { ok = 0; break; }
+        const double L0 = W00 * B0 + W01 * B1;
+        qc[k][0] = (float)(S.lines[k][0] + L0 * A00);
+        qc[k][1] = (float)(S.lines[k][1] + L0 * A10);
+      }
+      if (ok) {
+        float area = 0, len[3], pp;
+        for (int k = 0; k < 3; k++) {
+          const int a2 = k, b2 = (k + 1) % 3;
+          len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
         }
-        float qc[4][2];
-        ok = 1;
-        for (int k = 0; k < 4; k++) {
-          const int k1 = (k + 1) & 3;
-          const double A00 = lines[k][3], A01 = -lines[k1][3];
-          const double A10 = -lines[k][2], A11 = lines[k1][2];
-          const double B0 = -lines[k][0] + lines[k1][0];
-          const double B1 = -lines[k][1] + lines[k1][1];
-          const double det = A00 * A11 - A10 * A01;
-          const double W00 = A11 / det, W01 = -A01 / det;
-          if (fabs(det) < 0.001) { ok = 0; break; }
-          const double L0 = W00 * B0 + W01 * B1;
-          qc[k][0] = (float)(lines[k][0] + L0 * A00);
-          qc[k][1] = (float)(lines[k][1] + L0 * A10);
+        pp = (len[0] + len[1] + len[2]) / 2;
+        area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+        const int idxs[4] = {2, 3, 0, 2};
+        for (int k = 0; k < 3; k++) {
+          const int a2 = idxs[k], b2 = idxs[k + 1];
+          len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
         }
-        if (ok) {
-          float area = 0, len[3], pp;
-          for (int k = 0; k < 3; k++) {
-            const int a2 = k, b2 = (k + 1) % 3;
-            len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
-          }
-          pp = (len[0] + len[1] + len[2]) / 2;
-          area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
-          const int idxs[4] = {2, 3, 0, 2};
-          for (int k = 0; k < 3; k++) {
-            const int a2 = idxs[k], b2 = idxs[k + 1];
-            len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
-          }
-          pp = (len[0] + len[1] + len[2]) / 2;
-          area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
-          if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
-        }
-        if (ok) {
-          for (int k = 0; k < 4; k++) {
-            const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
-            const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
-            const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
-            const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
-            if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) { ok = 0; break; }
-          }
-        }
-        if (ok) {
-          for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
-            qc[k][0] = (qc[k][0] - 0.5f) * 2.0f + 0.5f;
-            qc[k][1] = (qc[k][1] - 0.5f) * 2.0f + 0.5f;
-            S.qc[k][0] = qc[k][0];
-            S.qc[k][1] = qc[k][1];
-            rec.corners[k][0] = qc[k][0];
-            rec.corners[k][1] = qc[k][1];
-          }
-        }
+        pp = (len[0] + len[1] + len[2]) / 2;
+        area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+        if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
+      }
+      for (int k = 0; ok && k < 4; k++) {
+        const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
+        const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
+        const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
+        const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
+        if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) ok = 0;
+      }
+      QuadCand qcand;
+      for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
+        const float x = ok ? (qc[k][0] - 0.5f) * 2.0f + 0.5f : 0.f;
+        const float y = ok ? (qc[k][1] - 0.5f) * 2.0f + 0.5f : 0.f;
+        rec.corners[k][0] = qcand.p[k][0] = x;
+        rec.corners[k][1] = qcand.p[k][1] = y;
       }
       rec.accepted = ok;
-      if (!ok)
-        for (int k = 0; k < 4; k++) rec.corners[k][0] = rec.corners[k][1] = 0.f;
       const uint32_t qi = atomicAdd(b.nquads + f, 1u);
       if (qi < (uint32_t)kMaxQuads) b.quads[(size_t)f * kMaxQuads + qi] = rec;
-      S.ok = ok;
+      if (ok && prm.diag_stop != 5) {
+        qcand.frame = (uint32_t)f;
+        qcand.rank = rank;
+        const uint32_t ci = atomicAdd(b.nqcand, 1u);
+        if (ci < b.qcand_cap) b.qcand[ci] = qcand;
+        else atomicOr(b.status + f, kStatusQuadsOverflow);
+      }
     }
     __syncthreads();
-    if (!S.ok) continue;
+  }
+}
 
-    // ---- RefineEdges (apriltag_detect.cu:405-564) -----------------------------
+// ---------------------------------------------------------------------------
+// K9b: one accepted quad per 64-lane workgroup iteration (persistent):
+// RefineEdges with UnDistort/ReDistort (apriltag_detect.cu:405-564),
+// homography (quad_update_homographies) and quad_decode (apriltag 3.x).
+// Order-dependent sums (line fit of the refined edge samples, gray models,
+// decision scores) run on one lane in the reference's order.
+// ---------------------------------------------------------------------------
+constexpr int kDecodeThreads = 64;
+constexpr int kMaxRefineSamples = 1536;
+
+struct DecodeShared {
+  double sx[kMaxRefineSamples], sy[kMaxRefineSamples];
+  float qc[4][2];
+  int nsamp[4], samp_off[4];
+  float enx[4], eny[4];
+  double lines[4][4];
+  double H[9];
+  double gmx[64], gmy[64], gmv[64];
+  int gmvalid[64];
+  double wC[3], bC[3];
+  double values[100];
+  uint64_t rcode;
+  double margin;
+  int ok;
+  uint32_t item;
+};
+
+__global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm) {
+  __shared__ DecodeShared S;
+  const int tid = threadIdx.x;
+  while (true) {
+    if (tid == 0) S.item = atomicAdd(b.qhead, 1u);
+    __syncthreads();
+    const uint32_t item = S.item;
+    const uint32_t nq = min(*b.nqcand, b.qcand_cap);
+    __syncthreads();
+    if (item >= nq) break;
+    const QuadCand qd = b.qcand[item];
+    const int f = (int)qd.frame;
+    const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
+    if (tid < 4) { S.qc[tid][0] = qd.p[tid][0]; S.qc[tid][1] = qd.p[tid][1]; }
+    __syncthreads();
     if (prm.refine_edges) {
       if (tid < 4) {
         const int a2 = tid, b2 = (tid + 1) & 3;
@@ -1290,15 +1395,11 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       __syncthreads();
       if (tid == 0) {
         int acc = 0;
-        for (int k = 0; k < 4; k++) {
-          S.samp_off[k] = acc;
-          acc += S.nsamp[k];
-        }
+        for (int k = 0; k < 4; k++) { S.samp_off[k] = acc; acc += S.nsamp[k]; }
       }
       __syncthreads();
-      const int total = S.samp_off[3] + S.nsamp[3];
-      const int cap = kSortCap / 2;
-      for (int t = tid; t < total && t < cap; t += kBlobThreads) {
+      const int total = min(S.samp_off[3] + S.nsamp[3], kMaxRefineSamples);
+      for (int t = tid; t < total; t += kDecodeThreads) {
         int edge = 0;
         while (edge < 3 && t >= S.samp_off[edge + 1]) edge++;
         const int s = t - S.samp_off[edge];
@@ -1309,14 +1410,12 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         const double x0 = alpha * S.qc[a2][0] + (1 - alpha) * S.qc[b2][0];
         const double y0 = alpha * S.qc[a2][1] + (1 - alpha) * S.qc[b2][1];
         double Mn = 0, Mcount = 0;
-        const double range = 3.0;
-        for (double nn = -range; nn <= range; nn += 0.25) {
-          const double grange = 1;
-          const int x1 = (int)(x0 + (nn + grange) * nx);
-          const int y1 = (int)(y0 + (nn + grange) * ny);
+        for (double nn = -3.0; nn <= 3.0; nn += 0.25) {
+          const int x1 = (int)(x0 + (nn + 1) * nx);
+          const int y1 = (int)(y0 + (nn + 1) * ny);
           if (x1 < 0 || x1 >= g.W || y1 < 0 || y1 >= g.H) continue;
-          const int x2 = (int)(x0 + (nn - grange) * nx);
-          const int y2 = (int)(y0 + (nn - grange) * ny);
+          const int x2 = (int)(x0 + (nn - 1) * nx);
+          const int y2 = (int)(y0 + (nn - 1) * ny);
           if (x2 < 0 || x2 >= g.W || y2 < 0 || y2 >= g.H) continue;
           const int g1 = gray[(size_t)y1 * g.W + x1], g2 = gray[(size_t)y2 * g.W + x2];
           if (g1 < g2) continue;
@@ -1331,15 +1430,15 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
           by = y0 + n0 * ny;
           undistort(prm, &bx, &by);
         }
-        S.u.smp.sx[t] = bx;
-        S.u.smp.sy[t] = by;
+        S.sx[t] = bx;
+        S.sy[t] = by;
       }
       __syncthreads();
       if (tid < 4) {
         double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
         const int o = S.samp_off[tid];
-        for (int s = 0; s < S.nsamp[tid] && o + s < cap; s++) {
-          const double bx = S.u.smp.sx[o + s], by = S.u.smp.sy[o + s];
+        for (int s = 0; s < S.nsamp[tid] && o + s < kMaxRefineSamples; s++) {
+          const double bx = S.sx[o + s], by = S.sy[o + s];
           if (isnan(bx)) continue;
           Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
         }
@@ -1375,6 +1474,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       }
       __syncthreads();
     }
+    if (prm.diag_stop == 6) continue;
     // ---- homography (quad_update_homographies / homography_compute2) -----------
     if (tid == 0) {
       double corr[4][4];
@@ -1396,8 +1496,8 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     }
     __syncthreads();
     if (!S.ok) continue;
-    // ---- quad_decode: border gray models ----------------------------------------
-    if (tid < 64) {
+    // ---- quad_decode: border gray models (8 patterns x 8 samples = 64 lanes) ----
+    {
       const int pidx = tid >> 3, i = tid & 7;
       const float wab = 8.0f;
       const float pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0, 1, 0}, {wab + 0.5f, .5f, 0, 1, 1},
@@ -1414,27 +1514,23 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       S.gmvalid[tid] = !(ix < 0 || iy < 0 || ix >= g.W || iy >= g.H);
       S.gmv[tid] = S.gmvalid[tid] ? (double)gray[(size_t)iy * g.W + ix] : 0.0;
     }
-    for (int t = tid; t < 100; t += kBlobThreads) S.values[t] = 0;
+    for (int t = tid; t < 100; t += kDecodeThreads) S.values[t] = 0;
     __syncthreads();
-    GrayModel wm, bm;
     if (tid == 0) {
+      GrayModel wm, bm;
       for (int k = 0; k < 3; k++) {
         wm.B[k] = bm.B[k] = 0;
         for (int j = 0; j < 3; j++) wm.A[k][j] = bm.A[k][j] = 0;
       }
       for (int t = 0; t < 64; t++) {
         if (!S.gmvalid[t]) continue;
-        const int is_white = ((t >> 3) & 1) == 0;
-        if (is_white) gm_add(wm, S.gmx[t], S.gmy[t], S.gmv[t]);
+        if (((t >> 3) & 1) == 0) gm_add(wm, S.gmx[t], S.gmy[t], S.gmv[t]);
         else gm_add(bm, S.gmx[t], S.gmy[t], S.gmv[t]);
       }
       gm_solve(wm);
       gm_solve(bm);
       S.ok = !(gm_interp(wm, 0, 0) - gm_interp(bm, 0, 0) < 0);
-      for (int k = 0; k < 3; k++) {
-        S.red_f64[k] = wm.C[k];
-        S.lines[0][k] = bm.C[k];
-      }
+      for (int k = 0; k < 3; k++) { S.wC[k] = wm.C[k]; S.bC[k] = bm.C[k]; }
     }
     __syncthreads();
     if (!S.ok) continue;
@@ -1444,34 +1540,43 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
       double px, py;
       hproject(S.H, tagx, tagy, &px, &py);
-      // value_for_pixel (bilinear)
       const int x1 = (int)floor(px - 0.5), x2 = (int)ceil(px - 0.5);
       const double xx = px - 0.5 - x1;
       const int y1 = (int)floor(py - 0.5), y2 = (int)ceil(py - 0.5);
       const double yy = py - 0.5 - y1;
-      if (!(x1 < 0 || x2 >= g.W || y1 < 0 || y2 >= g.H)) {
+      if (!(x1 < 0 || x2 >= g.W || y1 < 0 || y2 >= g.H)) {  // value_for_pixel
         const double v = gray[(size_t)y1 * g.W + x1] * (1 - xx) * (1 - yy) + gray[(size_t)y1 * g.W + x2] * xx * (1 - yy) +
                          gray[(size_t)y2 * g.W + x1] * (1 - xx) * yy + gray[(size_t)y2 * g.W + x2] * xx * yy;
-        const double bth = S.lines[0][0] * tagx + S.lines[0][1] * tagy + S.lines[0][2];
-        const double wth = S.red_f64[0] * tagx + S.red_f64[1] * tagy + S.red_f64[2];
-        const double thresh = (bth + wth) / 2.0;
-        S.values[10 * (bity + 1) + bitx + 1] = v - thresh;
+        const double bth = S.bC[0] * tagx + S.bC[1] * tagy + S.bC[2];
+        const double wth = S.wC[0] * tagx + S.wC[1] * tagy + S.wC[2];
+        S.values[10 * (bity + 1) + bitx + 1] = v - (bth + wth) / 2.0;
       }
     }
     __syncthreads();
+    // sharpen (apriltag.c): each lane owns cells t, t+64
+    double shv[2];
+    for (int r = 0; r < 2; r++) {
+      const int t = tid + 64 * r;
+      shv[r] = 0;
+      if (t < 100) {
+        const int y = t / 10, x = t % 10;
+        const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
+        double acc = 0;
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) {
+            if ((y + i - 1) < 0 || (y + i - 1) > 9 || (x + j - 1) < 0 || (x + j - 1) > 9) continue;
+            acc += S.values[(y + i - 1) * 10 + (x + j - 1)] * kern[i * 3 + j];
+          }
+        shv[r] = acc;
+      }
+    }
+    __syncthreads();
+    for (int r = 0; r < 2; r++) {
+      const int t = tid + 64 * r;
+      if (t < 100) S.values[t] = S.values[t] + prm.decode_sharpening * shv[r];
+    }
+    __syncthreads();
     if (tid == 0) {
-      double sh[100];
-      const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
-      for (int y = 0; y < 10; y++)
-        for (int x = 0; x < 10; x++) {
-          sh[y * 10 + x] = 0;
-          for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-              if ((y + i - 1) < 0 || (y + i - 1) > 9 || (x + j - 1) < 0 || (x + j - 1) > 9) continue;
-              sh[y * 10 + x] += S.values[(y + i - 1) * 10 + (x + j - 1)] * kern[i * 3 + j];
-            }
-        }
-      for (int t = 0; t < 100; t++) S.values[t] = S.values[t] + prm.decode_sharpening * sh[t];
       float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
       uint64_t rcode = 0;
       for (int i = 0; i < 36; i++) {
@@ -1480,33 +1585,33 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         if (v > 0) { white_score = (float)(white_score + v); white_cnt++; rcode |= 1; }
         else { black_score = (float)(black_score - v); black_cnt++; }
       }
-      S.red_u64[0] = rcode;
-      S.red_f64[3] = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
-      S.best_code = 0xffffffffu;
+      S.rcode = rcode;
+      S.margin = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
     }
     __syncthreads();
+    // quick_decode_codeword: first rotation, then entry, within hamming <= 2
+    uint32_t bc = 0xffffffffu;
     {
-      // quick_decode_codeword: first rotation (then entry) within hamming <= 2
-      const uint64_t rcode = S.red_u64[0];
-      for (int t = tid; t < 4 * c_book.n; t += kBlobThreads) {
+      const uint64_t rcode = S.rcode;
+      for (int t = tid; t < 4 * c_book.n; t += kDecodeThreads) {
         const int rot = t / c_book.n, ent = t % c_book.n;
         uint64_t r = rcode;
         for (int k = 0; k < rot; k++) r = rotate90_36(r);
         const int hd = __popcll(r ^ c_book.code[ent]);
-        if (hd <= 2) atomicMin(&S.best_code, (uint32_t)((rot << 24) | (hd << 16) | ent));
+        if (hd <= 2) bc = min(bc, (uint32_t)((rot << 24) | (hd << 16) | ent));
       }
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
     }
-    __syncthreads();
     if (tid == 0) {
-      const float margin = (float)S.red_f64[3];
-      const uint32_t bc = S.best_code;
+      const float margin = (float)S.margin;
       if (margin >= 0 && bc != 0xffffffffu) {
         const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
         DevDetection d;
         d.id = c_book.id[ent];
         d.hamming = hd;
         d.decision_margin = margin;
-        d.blob_rank = (int32_t)rank;
+        d.blob_rank = (int32_t)qd.rank;
         const double kRotC[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
         const double kRotS[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
         const double R[9] = {kRotC[rot], -kRotS[rot], 0, kRotS[rot], kRotC[rot], 0, 0, 0, 1};
@@ -1582,6 +1687,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
   mark();
   hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
+  mark();
+  hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm);
   mark();
   return hipGetLastError();
 }
