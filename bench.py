@@ -149,15 +149,16 @@ def main():
     fps = total_frames / elapsed
 
     # per-frame latency: one frame at a time, HBM -> detections in host memory
-    lat_det = rva.GpuDetector(W, H, max_batch=1, device=local_rank)
-    for i in range(10):
-        lat_det.detect_device(base + (i % npool) * stride, stride, 1)
-    lat = []
+    lat = [0.0]
+    if args.latency_frames > 0:
+        lat_det = rva.GpuDetector(W, H, max_batch=1, device=local_rank)
+        for i in range(10):
+            lat_det.detect_device(base + (i % npool) * stride, stride, 1)
     for i in range(args.latency_frames):
-        t1 = time.perf_counter()
+        t1 = time.perf_counter()  # noqa: E501 (lat_det exists when latency_frames > 0)
         lat_det.detect_device(base + (i % npool) * stride, stride, 1)
         lat.append(time.perf_counter() - t1)
-    lat = np.array(lat) * 1e3
+    lat = np.array(lat[1:] if len(lat) > 1 else lat) * 1e3
 
     # per-stage GPU time (HIP events on the detector's stream), separate pass
     stages, stage_batches = {}, 0

@@ -1,0 +1,93 @@
+"""world_size-2 gloo tests of the multi-GPU data path (CPU, no GPU needed).
+
+The detector on each rank is stood in for by the CPU oracle (test harness
+only); what is under test is the sharding, the frame scatter from rank 0, the
+fixed-size detection records and the gather back to rank 0, plus the bench's
+max/sum timing reduction.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, nper, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import ao
+    from ros_vision_amd import multigpu, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    codes = dict(ao.family_entries())
+    src = None
+    if rank == 0:
+        frames = np.stack([synth.to_yuyv(synth.render_board(W, H, seed=100 + i, ntags=4, codes=codes)[0])
+                           for i in range(world * nper)])
+        src = torch.from_numpy(frames)
+    mine = multigpu.scatter_frames(dist, src, nper, (H, 2 * W), "cpu").numpy()
+    o = ao.Oracle(W, H)
+    dets = []
+    for f in mine:
+        o.detect(f, 0)
+        dets.append(o.detections())
+    packed = multigpu.pack_detections(dets, 16)
+    allp = multigpu.gather_detections(dist, packed, "cpu")
+    el, cnt = multigpu.reduce_max_sum(dist, 1.0 + rank, float(sum(len(d) for d in dets)), "cpu")
+    if rank == 0:
+        q.put((allp, el, cnt))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_detect_gather_world2(oracle_mod):
+    from ros_vision_amd import multigpu, synth
+    W, H, nper, world = 320, 240, 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, nper, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    allp, el, cnt = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert el == 2.0  # max over ranks
+    got = multigpu.unpack_detections(allp)
+    codes = dict(oracle_mod.family_entries())
+    o = oracle_mod.Oracle(W, H)
+    total = 0
+    for i in range(world * nper):
+        o.detect(synth.to_yuyv(synth.render_board(W, H, seed=100 + i, ntags=4, codes=codes)[0]), 0)
+        want = o.detections()
+        total += len(want)
+        assert [d["id"] for d in got[i]] == [d["id"] for d in want]
+        for a, b in zip(got[i], want):
+            assert np.array_equal(a["p"], b["p"]) and np.array_equal(a["H"], b["H"])
+    assert cnt == total
+
+
+def test_shard_range_covers_all():
+    from ros_vision_amd.multigpu import shard_range
+    for world in (1, 2, 4, 8):
+        for n in (1, 7, 8, 64):
+            seen = []
+            for r in range(world):
+                lo, hi = shard_range(r, world, n)
+                seen.extend(range(lo, hi))
+            assert seen == list(range(n))

@@ -145,11 +145,18 @@ def test_cpu_oracle_stage_invariants(oracle_mod):
     assert set(np.unique(thr)) <= {0, 127, 255}
     lab = o.labels()
     sizes = o.sizes()
-    # every non-127 pixel's label is the minimum node id of its component => label <= own index
-    idx = np.arange(lab.size).reshape(lab.shape)
+    # labels are component roots: every live pixel's label carries the component's pixel count,
+    # and a root label is the min node id, so it never exceeds the pixel's own node id
+    # (fg node = top-left pixel of the 2x2 block, bg nodes = bottom-left / bottom-right pixel)
     live = thr != 127
-    assert np.all(lab[live] <= idx[live])
     assert sizes.sum() == np.count_nonzero(live)
+    assert np.all(sizes[lab[live]] > 0)
+    H2, W2 = thr.shape
+    rr, cc = np.mgrid[0:H2, 0:W2]
+    fg_node = (rr // 2 * 2) * W2 + (cc // 2 * 2)
+    bg_node = (rr // 2 * 2 + 1) * W2 + (cc // 2 * 2) + (cc % 2)
+    node = np.where(thr == 255, fg_node, bg_node)
+    assert np.all(lab[live] <= node[live])
     # sorted boundary points: rep01 non-decreasing (P2), rep0 < rep1
     p = o.sorted_points()
     r01 = p >> np.uint64(24)

@@ -1,0 +1,62 @@
+"""Generate tests/golden/vectors.json: oracle outputs on the committed inputs.
+
+Inputs are the reference's own fixtures (tests/golden/*_y.png, decoded from
+test/data/*.jpg by tools/make_golden_images.py) and seeded synthetic boards
+(ros_vision_amd/synth.py).  Per case we store per-stage digests (threshold
+plane, labels, sizes, sorted boundary points, sorted index points), counts and
+the final detections.  tests/test_golden.py checks the oracle still reproduces
+them and tests/test_gpu_parity.py checks the HIP path against them.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+from PIL import Image
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import ao  # noqa: E402
+from ros_vision_amd import synth  # noqa: E402
+
+
+def cases():
+    codes = dict(ao.family_entries())
+    g = os.path.join(ROOT, "tests", "golden")
+    yield "colorimage", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_y.png"))
+    yield "colorimage_notags", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_notags_y.png"))
+    yield "c1_640x480", 640, 480, 0, synth.to_yuyv(synth.render_board(640, 480, seed=766, ntags=4,
+                                                                       ids=[0, 1, 2, 554], codes=codes)[0])
+    for f in range(3):
+        yield "c2_720p_f%d" % f, 1280, 720, 0, synth.stream_frame(1280, 720, f, codes=codes)[0]
+    yield "c4_1080p", 1920, 1080, 0, synth.to_yuyv(synth.render_board(1920, 1080, seed=4242, ntags=24,
+                                                                       codes=codes)[0])
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
+
+
+def run_case(W, H, fmt, frame):
+    o = ao.Oracle(W, H)
+    o.detect(frame, fmt)
+    pts = o.sorted_points()
+    return {
+        "thr": digest(o.thresholded()), "labels": digest(o.labels()), "sizes": digest(o.sizes()),
+        "points_sorted": digest(np.sort(pts)), "num_points": int(pts.size), "num_pairs": o.num_pairs(),
+        "index_points": digest(o.sorted_index_points()), "num_index_points": int(o.sorted_index_points().size),
+        "valid_fitquads": sum(int(f.valid) for f in o.fitquads()), "quads": len(o.quads()),
+        "detections": [{"id": d["id"], "hamming": d["hamming"], "decision_margin": float(d["decision_margin"]),
+                        "c": d["c"].tolist(), "p": d["p"].tolist(), "H": d["H"].ravel().tolist()}
+                       for d in o.detections()],
+    }
+
+
+if __name__ == "__main__":
+    out = {}
+    for name, W, H, fmt, frame in cases():
+        out[name] = dict(width=W, height=H, fmt=fmt, **run_case(W, H, fmt, frame))
+        print(name, [d["id"] for d in out[name]["detections"]])
+    json.dump(out, open(os.path.join(ROOT, "tests", "golden", "vectors.json"), "w"), indent=1)
