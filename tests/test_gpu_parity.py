@@ -122,3 +122,38 @@ def test_device_resident_frames(gpu, oracle_mod):
         orc = oracle_mod.Oracle(1280, 720)
         orc.detect(frames[i], 0)
         assert compare_detections(res[i], orc.detections()) == []
+
+
+def _golden():
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return json.load(open(os.path.join(root, "tests", "golden", "vectors.json")))
+
+
+@pytest.mark.parametrize("name", sorted(_golden()))
+def test_gpu_matches_committed_golden(gpu, name):
+    """HIP path vs the committed golden vectors: stage digests bit-exact,
+    ids/hamming exact, floats within 1e-4."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import make_golden_vectors as mg
+    want = _golden()[name]
+    W, H, fmt, frame = {n: (W, H, f, fr) for n, W, H, f, fr in mg.cases()}[name]
+    det = gpu.GpuDetector(W, H)
+    dets = det.detect(frame, fmt)
+    assert mg.digest(det.copy_thresholded()) == want["thr"]
+    assert mg.digest(det.copy_union_markers()) == want["labels"]
+    assert mg.digest(det.copy_union_markers_size()) == want["sizes"]
+    assert mg.digest(np.sort(det.copy_points())) == want["points_sorted"]
+    assert det.num_pairs() == want["num_pairs"]
+    assert mg.digest(det.copy_blob_points()) == want["index_points"]
+    assert [d.id for d in dets] == [d["id"] for d in want["detections"]]
+    for a, b in zip(dets, want["detections"]):
+        assert a.hamming == b["hamming"]
+        assert abs(a.decision_margin - b["decision_margin"]) <= 1e-4
+        assert np.allclose(a.p, np.array(b["p"]), atol=1e-4) and np.allclose(a.c, np.array(b["c"]), atol=1e-4)
+        assert np.allclose(a.H.ravel(), np.array(b["H"]), atol=1e-4)
+        assert np.array_equal(np.floor(a.p), np.floor(np.array(b["p"])))
