@@ -116,8 +116,10 @@ enum {
   AT_STAGE_NUM_POINTS = 5,  /* u32 count of boundary points N_c */
   AT_STAGE_NUM_PAIRS = 6,   /* u32 count of blob pairs N_q */
   AT_STAGE_QUADS = 7,       /* at_quad_record[] of fitted quads (see below) */
-  AT_STAGE_POINTS = 8,      /* u64 QuadBoundaryPoint keys, grouped by pair rank */
-  AT_STAGE_BLOB_POINTS = 9  /* u64 IndexPoint keys of selected blobs, sorted (blob, theta) */
+  AT_STAGE_POINTS = 8,      /* u64 QuadBoundaryPoint keys, in emission order (unordered) */
+  AT_STAGE_BLOB_POINTS = 9, /* u64 IndexPoint keys of selected blobs, sorted (blob, theta) */
+  AT_STAGE_NUM_PAIR_ENTRIES = 10, /* u32 per-tile pair-histogram entries (diagnostic) */
+  AT_STAGE_PROBE = 11       /* u64[256] kernel phase clock stamps when AT_PHASE_PROBE is set (diagnostic) */
 };
 long long at_debug_copy(at_detector *d, int stage, int frame, void *dst, size_t bytes);
 

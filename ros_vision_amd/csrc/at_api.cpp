@@ -175,6 +175,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.fx = cam->fx; p.fy = cam->fy; p.cx = cam->cx; p.cy = cam->cy;
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
+  p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
 
   auto fail = [&](int code) {
     at_destroy(d);
@@ -213,6 +214,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.size = (uint32_t*)dalloc(B * nd * 4);
   b.pts = (uint64_t*)dalloc(B * g.cap_pts * 8);
   b.grp = (uint64_t*)dalloc(B * g.cap_pts * 8);
+  b.pent_key = (uint64_t*)dalloc(B * kPairEntCap * 8);
+  b.pent_cnt = (uint32_t*)dalloc(B * kPairEntCap * 4);
   b.ht_key = (uint64_t*)dalloc(B * kHashSlots * 8);
   b.ht_cnt = (uint32_t*)dalloc(B * kHashSlots * 4);
   b.ht_rank = (uint32_t*)dalloc(B * kHashSlots * 4);
@@ -222,9 +225,11 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.pair_off = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.pair_sel = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.work = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.work_small = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.probe = (uint64_t*)dalloc(kProbeWords * 8);
   b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
   b.quads = (QuadRecord*)dalloc(B * kMaxQuads * sizeof(QuadRecord));
-  d->ctrl_words = 5 * B + 4;
+  d->ctrl_words = 6 * B + 8;
   d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
   b.npts = d->d_ctrl;
   b.npairs = d->d_ctrl + B;
@@ -235,12 +240,16 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.workhead = d->d_ctrl + 5 * B + 1;
   b.nqcand = d->d_ctrl + 5 * B + 2;
   b.qhead = d->d_ctrl + 5 * B + 3;
+  b.npent = d->d_ctrl + 5 * B + 4;
+  b.nwork_small = d->d_ctrl + 6 * B + 4;
+  b.workhead_small = d->d_ctrl + 6 * B + 5;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
-  const size_t nw = (size_t)d->nblobwg;
-  b.s_i32 = (int32_t*)dalloc(nw * 3 * kSortCap * 4);
-  b.s_i64 = (int64_t*)dalloc(nw * 3 * kSortCap * 8);
-  b.s_f64 = (double*)dalloc(nw * 2 * kSortCap * 8);
+  // blob scratch: large teams (nblobwg x kSortCap) and small teams (8 x nblobwg x kSmallBlob) share it
+  const size_t nw = std::max((size_t)d->nblobwg * kSortCap, (size_t)d->nblobwg * 8 * kSmallBlob);
+  b.s_i32 = (int32_t*)dalloc(nw * 3 * 4);
+  b.s_i64 = (int64_t*)dalloc(nw * 3 * 8);
+  b.s_f64 = (double*)dalloc(nw * 2 * 8);
   if (oom) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
@@ -488,6 +497,11 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       if (bytes < 4) return AT_E_INVALID;
       memcpy(dst, &d->h_ctrl[B + frame], 4);
       return 4;
+    case AT_STAGE_NUM_PAIR_ENTRIES:
+      if (bytes < 4) return AT_E_INVALID;
+      memcpy(dst, &d->h_ctrl[5 * B + 4 + frame], 4);
+      return 4;
+    case AT_STAGE_PROBE: src = d->d.probe; n = kProbeWords * 8; break;
     case AT_STAGE_QUADS: {
       const uint32_t nq = std::min<uint32_t>(d->h_ctrl[3 * B + frame], (uint32_t)kMaxQuads);
       std::vector<QuadRecord> q(nq);

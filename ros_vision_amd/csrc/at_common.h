@@ -9,19 +9,21 @@ namespace at {
 
 // ---- capacities -----------------------------------------------------------
 constexpr int kCclTile = 32;           // CCL tile edge in decimated pixels (16x16 2x2-blocks)
-constexpr int kHashSlots = 16384;      // per-frame open-addressing table of blob pairs
-constexpr int kHashBits = 14;
+constexpr int kHashSlots = 8192;       // per-frame open-addressing table of blob pairs (<= 50% full)
+constexpr int kHashBits = 13;
+constexpr int kPairEntCap = 65536;     // per-frame (tile, pair, count) entries k_boundary hands to k_pairs
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kMaxDets = 128;          // candidate detections per frame
 constexpr int kMaxQuads = 2048;        // fitted-quad debug records per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
+constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wave-per-blob
 constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
-constexpr int kNumStages = 9;
+constexpr int kNumStages = 10;
 constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final", "k_boundary",
-                                                 "k_pairs", "k_group",   "k_blob",       "k_decode"};
+                                                 "k_pairs", "k_group",   "k_blob_small", "k_blob",       "k_decode"};
 
 // ---- per-frame status bits -------------------------------------------------
 constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs
@@ -51,7 +53,9 @@ struct Params {
   int refine_edges;
   double fx, fy, cx, cy, k1, k2, p1, p2, k3;
   int diag_stop;  // diagnostics only (AT_DIAG_BLOB_STOP): k_blob returns after phase N; 0 = full
+  int probe;      // diagnostics only (AT_PHASE_PROBE): kernels stamp phase clocks into DevBufs::probe
 };
+constexpr int kProbeWords = 256;
 
 // One detection candidate as produced on the device (before reconcile).
 struct DevDetection {
@@ -87,7 +91,10 @@ struct DevBufs {
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][cap_pts]   boundary points, emission order
   uint64_t* grp;      // [B][cap_pts]   boundary points grouped by pair rank
-  uint64_t* ht_key;   // [B][kHashSlots]
+  uint64_t* pent_key; // [B][kPairEntCap]  per-tile pair histogram entries (rep01)
+  uint32_t* pent_cnt; // [B][kPairEntCap]
+  uint32_t* npent;    // [B] (in the control block)
+  uint64_t* ht_key;   // [B][kHashSlots]  written whole by k_pairs
   uint32_t* ht_cnt;   // [B][kHashSlots]
   uint32_t* ht_rank;  // [B][kHashSlots]
   uint32_t* ht_off;   // [B][kHashSlots]
@@ -95,7 +102,8 @@ struct DevBufs {
   uint32_t* pair_cnt; // [B][kMaxPairs]
   uint32_t* pair_off; // [B][kMaxPairs]
   uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair
-  uint32_t* work;     // [B*kMaxPairs]   (frame << 16) | rank of candidate pairs
+  uint32_t* work;     // [B*kMaxPairs]   (frame << 16) | rank of candidate pairs (> kSmallBlob points)
+  uint32_t* work_small; // [B*kMaxPairs] same, <= kSmallBlob points
   DevDetection* dets; // [B][kMaxDets]
   QuadRecord* quads;  // [B][kMaxQuads]
   // control block (zeroed every batch)
@@ -106,6 +114,9 @@ struct DevBufs {
   uint32_t* status;   // [B]
   uint32_t* nwork;    // [1]
   uint32_t* workhead; // [1]
+  uint64_t* probe;    // [kProbeWords] phase clock stamps (diagnostics)
+  uint32_t* nwork_small;    // [1]
+  uint32_t* workhead_small; // [1]
   uint32_t* nqcand;   // [1]
   uint32_t* qhead;    // [1]
   QuadCand* qcand;    // [qcand_cap]

@@ -177,21 +177,6 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
   __shared__ uint32_t s_par[768];
   __shared__ uint32_t s_cnt[768];
 
-  // zero this tile's share of the frame's pair hash table (used by k_boundary)
-  {
-    const int ntiles = g.CTX * g.CTY;
-    const int tile = blockIdx.y * g.CTX + blockIdx.x;
-    const int per = (kHashSlots + ntiles - 1) / ntiles;
-    const int s0 = tile * per;
-    for (int i = tid; i < per; i += 256) {
-      const int s = s0 + i;
-      if (s < kHashSlots) {
-        b.ht_key[(size_t)f * kHashSlots + s] = 0;
-        b.ht_cnt[(size_t)f * kHashSlots + s] = 0;
-      }
-    }
-  }
-
   // unfiltered tile min/max for tile rows ty0-2..ty0+8, cols tx0-2..tx0+9
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   for (int i = tid; i < 11 * 12; i += 256) {
@@ -455,20 +440,6 @@ __device__ __forceinline__ uint64_t make_qbp(uint32_t rep0, uint32_t rep1, uint3
          ((uint64_t)(y & 0x3ff) << 4) | ((uint64_t)(b2w ? 1 : 0) << 3) | (uint64_t)(dxy & 3);
 }
 
-__device__ uint32_t ht_slot_insert(uint64_t* keys, uint64_t key) {
-  uint32_t s = (uint32_t)mix_hash(key);
-  for (int probe = 0; probe < kHashSlots; probe++) {
-    const uint64_t k = keys[s];
-    if (k == key) return s;
-    if (k == 0) {
-      const uint64_t prev = atomicCAS((unsigned long long*)(keys + s), 0ull, (unsigned long long)key);
-      if (prev == 0 || prev == key) return s;
-    }
-    s = (s + 1) & (kHashSlots - 1);
-  }
-  return 0xffffffffu;
-}
-
 __device__ uint32_t ht_slot_find(const uint64_t* keys, uint64_t key) {
   uint32_t s = (uint32_t)mix_hash(key);
   for (int probe = 0; probe < kHashSlots; probe++) {
@@ -510,99 +481,126 @@ __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uin
   return false;
 }
 
-// One 256-thread workgroup covers 64x4 interior pixels (up to 1024 points).
-// Points are compacted with a block scan and ONE global atomic per workgroup;
-// the pair histogram is aggregated in an LDS hash table (lane runs first) and
-// flushed with one global atomic per distinct pair per workgroup.
+// One 256-thread workgroup covers a 64 x (4*kBndRows) tile of interior pixels.
+// Points are staged in LDS (wave-aggregated LDS atomics) and written out with
+// ONE global atomic per workgroup; the pair histogram is aggregated in an LDS
+// hash table (runs of equal pairs in consecutive lanes first) and appended to
+// the frame's pair-entry list with one more global atomic per workgroup.
+constexpr int kBndRows = 4;
+constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel
+
+__device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key, uint32_t cnt) {
+  const uint32_t o = atomicAdd(b.npent + f, 1u);
+  if (o < (uint32_t)kPairEntCap) {
+    b.pent_key[(size_t)f * kPairEntCap + o] = key;
+    b.pent_cnt[(size_t)f * kPairEntCap + o] = cnt;
+  } else {
+    atomicOr(b.status + f, kStatusHashFull);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
-  __shared__ uint32_t s_wsum[4];
-  __shared__ uint32_t s_base;
+  __shared__ uint64_t s_pts[kBndPts];
+  __shared__ uint32_t s_npts, s_nent, s_base, s_ebase;
   const int f = blockIdx.z;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   for (int i = tid; i < kLdsPairSlots; i += 256) {
     s_pkey[i] = 0;
     s_pcnt[i] = 0;
   }
+  if (tid == 0) { s_npts = 0; s_nent = 0; }
+  __syncthreads();  // LDS table initialised
   const int x = 1 + blockIdx.x * 64 + threadIdx.x;
-  const int y = 1 + blockIdx.y * 4 + threadIdx.y;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   const uint8_t* thr = b.thr + fo;
   const uint32_t* lab = b.lab + fo;
   const uint32_t* size = b.size + fo;
   const int Wd = g.Wd;
-  uint64_t pk[4] = {0, 0, 0, 0};
-  if (x <= g.Wd - 2 && y <= g.Hd - 2) {
-    const size_t i0 = (size_t)y * Wd + x;
-    const uint8_t v0 = thr[i0];
-    const uint32_t rep0 = lab[i0];
-    if (v0 != 127 && size[rep0] >= 25) {
-      const uint8_t vr = thr[i0 + 1], vd = thr[i0 + Wd], vdr = thr[i0 + Wd + 1], vdl = thr[i0 + Wd - 1],
-                    vl = thr[i0 - 1];
-      const uint32_t lr = lab[i0 + 1], ld = lab[i0 + Wd], ldr = lab[i0 + Wd + 1], ldl = lab[i0 + Wd - 1],
-                     ll = lab[i0 - 1];
-      if (v0 + vr == 255 && size[lr] >= 25) pk[0] = make_qbp(rep0, lr, x, y, 0, vr > v0);
-      if (v0 + vdr == 255 && size[ldr] >= 25) pk[1] = make_qbp(rep0, ldr, x, y, 1, vdr > v0);
-      if (v0 + vd == 255 && size[ld] >= 25) pk[2] = make_qbp(rep0, ld, x, y, 2, vd > v0);
-      bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && size[ll] >= 25 && size[ld] >= 25;
-      if (!dedup && v0 + vdl == 255 && size[ldl] >= 25) pk[3] = make_qbp(rep0, ldl, x, y, 3, vdl > v0);
-    }
-  }
-  __syncthreads();  // LDS table initialised
   const uint32_t lane = lane_id();
-  uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
-  uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
-  uint32_t npk = 0;
-#pragma unroll
-  for (int dir = 0; dir < 4; dir++) {
-    const bool has = pk[dir] != 0;
-    npk += has;
-    const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
-    const uint64_t prev = __shfl_up(r01, 1);
-    const bool same = has && lane > 0 && prev == r01;
-    const uint64_t same_mask = __ballot(same);
-    if (has && !same) {
-      const uint32_t len = run_len(same_mask, lane);
-      if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) {
-        const uint32_t s = ht_slot_insert(ht_key, r01);
-        if (s == 0xffffffffu) atomicOr(b.status + f, kStatusHashFull);
-        else atomicAdd(ht_cnt + s, len);
+  for (int r = 0; r < kBndRows; r++) {
+    const int y = 1 + (blockIdx.y * kBndRows + r) * 4 + threadIdx.y;
+    uint64_t pk[4] = {0, 0, 0, 0};
+    if (x <= g.Wd - 2 && y <= g.Hd - 2) {
+      const size_t i0 = (size_t)y * Wd + x;
+      const uint8_t v0 = thr[i0];
+      if (v0 != 127) {
+        const uint32_t rep0 = lab[i0];
+        if (size[rep0] >= 25) {
+          const uint8_t vr = thr[i0 + 1], vd = thr[i0 + Wd], vdr = thr[i0 + Wd + 1], vdl = thr[i0 + Wd - 1],
+                        vl = thr[i0 - 1];
+          const uint32_t lr = lab[i0 + 1], ld = lab[i0 + Wd], ldr = lab[i0 + Wd + 1], ldl = lab[i0 + Wd - 1],
+                         ll = lab[i0 - 1];
+          if (v0 + vr == 255 && size[lr] >= 25) pk[0] = make_qbp(rep0, lr, x, y, 0, vr > v0);
+          if (v0 + vdr == 255 && size[ldr] >= 25) pk[1] = make_qbp(rep0, ldr, x, y, 1, vdr > v0);
+          if (v0 + vd == 255 && size[ld] >= 25) pk[2] = make_qbp(rep0, ld, x, y, 2, vd > v0);
+          const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && size[ll] >= 25 && size[ld] >= 25;
+          if (!dedup && v0 + vdl == 255 && size[ldl] >= 25) pk[3] = make_qbp(rep0, ldl, x, y, 3, vdl > v0);
+        }
       }
     }
-  }
-  // block-wide exclusive scan of the per-thread point counts
-  uint32_t incl = npk;
+    uint32_t npk = 0;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d);
-    if (lane >= (uint32_t)d) incl += v;
-  }
-  const int w = tid >> 6;
-  if (lane == 63) s_wsum[w] = incl;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (int i = 0; i < w; i++) wbase += s_wsum[i];
-  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  if (tid == 0) s_base = total ? atomicAdd(b.npts + f, total) : 0u;
-  __syncthreads();
-  uint32_t pos = s_base + wbase + incl - npk;
-  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
-#pragma unroll
-  for (int dir = 0; dir < 4; dir++) {
-    if (pk[dir]) {
-      if (pos < (uint32_t)g.cap_pts) pts[pos] = pk[dir];
-      else atomicOr(b.status + f, kStatusPointsOverflow);
-      pos++;
+    for (int dir = 0; dir < 4; dir++) {
+      const bool has = pk[dir] != 0;
+      npk += has;
+      const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
+      const uint64_t prev = __shfl_up(r01, 1);
+      const bool same = has && lane > 0 && prev == r01;
+      const uint64_t same_mask = __ballot(same);
+      if (has && !same) {
+        const uint32_t len = run_len(same_mask, lane);
+        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) bnd_spill(b, f, r01, len);  // LDS table full
+      }
     }
+    // wave-aggregated append of the points into the LDS staging buffer
+    uint32_t incl = npk;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= (uint32_t)d) incl += v;
+    }
+    const uint32_t wtot = __shfl(incl, 63);
+    uint32_t wbase = 0;
+    if (lane == 0 && wtot) wbase = atomicAdd(&s_npts, wtot);
+    wbase = __shfl(wbase, 0);
+    uint32_t pos = wbase + incl - npk;
+#pragma unroll
+    for (int dir = 0; dir < 4; dir++)
+      if (pk[dir]) s_pts[pos++] = pk[dir];
   }
-  // flush the workgroup's pair histogram
+  __syncthreads();
+  const uint32_t total = s_npts;
+  if (tid == 0) s_base = total ? atomicAdd(b.npts + f, total) : 0u;
+  // count the distinct pairs of the tile
+  uint32_t mine = 0;
+  for (int i = tid; i < kLdsPairSlots; i += 256) mine += s_pkey[i] != 0;
+  uint32_t wn = mine;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) wn += __shfl_xor(wn, d);
+  if (lane == 0 && wn) atomicAdd(&s_nent, wn);
+  __syncthreads();
+  const uint32_t nent = s_nent;
+  if (tid == 0) s_ebase = nent ? atomicAdd(b.npent + f, nent) : 0u;
+  if (tid == 0) s_nent = 0;
+  __syncthreads();
+  const uint32_t base = s_base, ebase = s_ebase;
+  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
+  for (uint32_t i = tid; i < total; i += 256) {
+    if (base + i < (uint32_t)g.cap_pts) pts[base + i] = s_pts[i];
+    else atomicOr(b.status + f, kStatusPointsOverflow);
+  }
   for (int i = tid; i < kLdsPairSlots; i += 256) {
     const uint64_t k = s_pkey[i];
     if (k) {
-      const uint32_t s = ht_slot_insert(ht_key, k);
-      if (s == 0xffffffffu) atomicOr(b.status + f, kStatusHashFull);
-      else atomicAdd(ht_cnt + s, s_pcnt[i]);
+      const uint32_t o = ebase + atomicAdd(&s_nent, 1u);
+      if (o < (uint32_t)kPairEntCap) {
+        b.pent_key[(size_t)f * kPairEntCap + o] = k;
+        b.pent_cnt[(size_t)f * kPairEntCap + o] = s_pcnt[i];
+      } else {
+        atomicOr(b.status + f, kStatusHashFull);
+      }
     }
   }
 }
@@ -633,19 +631,52 @@ __device__ void block_bitonic_sort(T* s, int n) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g) {
+__global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
+  auto stamp = [&](int i) {
+    if (probe && f == 0 && tid == 0) b.probe[i] = wall_clock64();
+  };
+  stamp(0);
+  __shared__ uint64_t t_key[kHashSlots];
+  __shared__ uint32_t t_cnt[kHashSlots];
   __shared__ uint64_t s_list[kMaxPairs];
   __shared__ uint32_t s_cnt[kMaxPairs];
-  __shared__ uint32_t s_n;
+  __shared__ uint32_t s_n, s_full;
   __shared__ uint32_t s_wsum[16];
-  const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
-  const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
-  if (tid == 0) s_n = 0;
+  for (int i = tid; i < kHashSlots; i += 1024) {
+    t_key[i] = 0;
+    t_cnt[i] = 0;
+  }
+  if (tid == 0) { s_n = 0; s_full = 0; }
   __syncthreads();
+  // merge the per-tile pair histograms of k_boundary in LDS
+  const uint32_t total = min(b.npent[f], (uint32_t)kPairEntCap);
+  for (uint32_t i = tid; i < total; i += 1024) {
+    const uint64_t key = b.pent_key[(size_t)f * kPairEntCap + i];
+    const uint32_t cnt = b.pent_cnt[(size_t)f * kPairEntCap + i];
+    uint32_t h = (uint32_t)mix_hash(key);
+    bool done = false;
+    for (int probe = 0; probe < kHashSlots && !done; probe++) {
+      const uint64_t k = t_key[h];
+      if (k == key) {
+        atomicAdd(&t_cnt[h], cnt);
+        done = true;
+      } else if (k == 0) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&t_key[h], 0ull, (unsigned long long)key);
+        if (prev == 0 || prev == key) {
+          atomicAdd(&t_cnt[h], cnt);
+          done = true;
+        }
+      }
+      h = (h + 1) & (kHashSlots - 1);
+    }
+    if (!done) s_full = 1;
+  }
+  __syncthreads();
+  stamp(1);
   for (int s = tid; s < kHashSlots; s += 1024) {
-    const uint64_t k = ht_key[s];
+    const uint64_t k = t_key[s];
     if (k) {
       const uint32_t i = atomicAdd(&s_n, 1u);
       if (i < kMaxPairs) s_list[i] = (k << kHashBits) | (uint64_t)s;
@@ -654,18 +685,24 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g) {
   __syncthreads();
   const uint32_t n = s_n;
   if (tid == 0) b.npairs[f] = n;
-  if (n > (uint32_t)kMaxPairs) {
-    if (tid == 0) atomicOr(b.status + f, kStatusPairsOverflow);
+  if (n > (uint32_t)kMaxPairs || s_full) {
+    if (tid == 0) atomicOr(b.status + f, s_full ? kStatusHashFull : kStatusPairsOverflow);
     return;
+  }
+  // the lookup table used by k_group: keys of every slot (0 = empty)
+  for (int s = tid; s < kHashSlots; s += 1024) {
+    b.ht_key[(size_t)f * kHashSlots + s] = t_key[s];
+    b.ht_cnt[(size_t)f * kHashSlots + s] = t_cnt[s];
   }
   int np2 = 64;
   while (np2 < (int)n) np2 <<= 1;
   for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
   __syncthreads();
+  stamp(2);
   block_bitonic_sort<uint64_t, 1024>(s_list, np2);
+  stamp(3);
   // counts in rank order, exclusive scan -> offsets
-  for (int i = tid; i < kMaxPairs; i += 1024)
-    s_cnt[i] = i < (int)n ? ht_cnt[s_list[i] & (kHashSlots - 1)] : 0u;
+  for (int i = tid; i < kMaxPairs; i += 1024) s_cnt[i] = i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u;
   __syncthreads();
   // each thread owns 4 consecutive ranks
   const int i0 = tid * 4;
@@ -685,6 +722,38 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g) {
   const uint32_t excl = wbase + incl - tsum;
   const uint32_t offs[4] = {excl, excl + c0, excl + c0 + c1, excl + c0 + c1 + c2};
   const uint32_t cs[4] = {c0, c1, c2, c3};
+  stamp(4);
+  // work-list appends: one global atomic per list per workgroup
+  bool take[4], small[4];
+  uint32_t nsl = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    take[k] = i0 + k < (int)n && cs[k] >= g.min_cluster && cs[k] <= g.max_cluster;
+    small[k] = cs[k] <= (uint32_t)kSmallBlob;
+    nsl += take[k] ? (small[k] ? 1u : 0x10000u) : 0u;
+  }
+  uint32_t winc = nsl;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(winc, d);
+    if (lane >= (uint32_t)d) winc += v;
+  }
+  __syncthreads();  // s_wsum reuse
+  if (lane == 63) s_wsum[tid >> 6] = winc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tot = 0;
+    for (int w = 0; w < 16; w++) {
+      const uint32_t t = s_wsum[w];
+      s_wsum[w] = tot;
+      tot += t;
+    }
+    s_n = (tot & 0xffff) ? atomicAdd(b.nwork_small, tot & 0xffff) : 0u;
+    s_full = (tot >> 16) ? atomicAdd(b.nwork, tot >> 16) : 0u;
+  }
+  __syncthreads();
+  const uint32_t wpre = s_wsum[tid >> 6] + winc - nsl;
+  uint32_t ps = s_n + (wpre & 0xffff), pl = s_full + (wpre >> 16);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
@@ -696,12 +765,13 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g) {
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
       b.pair_off[(size_t)f * kMaxPairs + i] = offs[k];
       b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
-      if (cs[k] >= g.min_cluster && cs[k] <= g.max_cluster) {
-        const uint32_t w = atomicAdd(b.nwork, 1u);
-        b.work[w] = ((uint32_t)f << 16) | (uint32_t)i;
+      if (take[k]) {
+        if (small[k]) b.work_small[ps++] = ((uint32_t)f << 16) | (uint32_t)i;
+        else b.work[pl++] = ((uint32_t)f << 16) | (uint32_t)i;
       }
     }
   }
+  stamp(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -870,6 +940,71 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total) {
 }
 
 
+// ---- team-generic primitives: a team is the whole 256-thread workgroup
+// (large blobs) or one 64-lane wave (small blobs, 4 independent teams per WG)
+template <int NT>
+__device__ __forceinline__ void team_sync() {
+  if constexpr (NT == 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ int team_rank() {
+  return NT == 64 ? (int)lane_id() : (int)threadIdx.x;
+}
+
+template <int NT, typename T, typename Op>
+__device__ T team_reduce(T v, Op op, T* s_tmp) {
+  if constexpr (NT == 64) {
+    return wave_reduce(v, op);
+  } else {
+    return block_reduce(v, op, s_tmp);
+  }
+}
+
+template <int NT, typename T>
+__device__ T team_incl_scan(T v, T* s_tmp, T* total) {
+  if constexpr (NT == 64) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const T u = __shfl_up(v, d);
+      if (lane >= (uint32_t)d) v = v + u;
+    }
+    *total = __shfl(v, 63);
+    return v;
+  } else {
+    return block_incl_scan(v, s_tmp, total);
+  }
+}
+
+template <typename T, int NT>
+__device__ void team_bitonic_sort(T* s, int n) {
+  const int r = team_rank<NT>();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = r; i < n; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const T a = s[i], c = s[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) {
+            s[i] = c;
+            s[ixj] = a;
+          }
+        }
+      }
+      team_sync<NT>();
+    }
+  }
+}
+
+
 __device__ void redistort(const Params& p, double* x, double* y) {
   const double xP = (*x - p.cx) / p.fx, yP = (*y - p.cy) / p.fy;
   const double rSq = xP * xP + yP * yP;
@@ -1000,8 +1135,9 @@ __device__ __forceinline__ LineFitOut fit_line_v(const Moments& m) {
   return o;
 }
 
+template <int CAP>
 struct BlobShared {
-  uint64_t keys[kSortCap];  // point sort keys, later peak keys
+  uint64_t keys[CAP];  // point sort keys, later peak keys
   double red_f64[4];
   int64_t red_i64[4];
   uint32_t red_u32[4];
@@ -1014,35 +1150,12 @@ struct BlobShared {
   double lines[4][4];
 };
 
-// K9a: one blob pair per workgroup iteration (persistent, work-list driven):
-// extents + SelectBlobs, theta sort, line-fit prefix sums, errors, filter,
-// peaks, FitQuads, UpdateFitQuads.  Accepted quads go to the decode list.
-__global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params prm) {
-  __shared__ BlobShared S;
-  const int tid = threadIdx.x;
+// Processes one work item (frame, pair rank) with a team of NT threads.
+template <int NT, int CAP>
+__device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<CAP>& S,
+                          const BlobScratch& P, uint32_t w) {
+  const int tid = team_rank<NT>();
   const uint32_t lane = lane_id();
-  BlobScratch P;
-  {
-    const size_t wg = blockIdx.x;
-    P.Mx = b.s_i32 + (wg * 3 + 0) * kSortCap;
-    P.My = b.s_i32 + (wg * 3 + 1) * kSortCap;
-    P.W = b.s_i32 + (wg * 3 + 2) * kSortCap;
-    P.Mxx = b.s_i64 + (wg * 3 + 0) * kSortCap;
-    P.Myy = b.s_i64 + (wg * 3 + 1) * kSortCap;
-    P.Mxy = b.s_i64 + (wg * 3 + 2) * kSortCap;
-    P.err = b.s_f64 + (wg * 2 + 0) * kSortCap;
-    P.filt = b.s_f64 + (wg * 2 + 1) * kSortCap;
-  }
-  if (tid == 0) S.nwork = *b.nwork;
-  __syncthreads();
-  const uint32_t nwork = S.nwork;
-  while (true) {
-    if (tid == 0) S.item = atomicAdd(b.workhead, 1u);
-    __syncthreads();
-    const uint32_t item = S.item;
-    __syncthreads();
-    if (item >= nwork) break;
-    const uint32_t w = b.work[item];
     const int f = (int)(w >> 16);
     const uint32_t rank = w & 0xffff;
     const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
@@ -1054,7 +1167,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
     int32_t sgx = 0, sgy = 0;
     int64_t spg = 0;
-    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+    for (uint32_t t = tid; t < n; t += NT) {
       const uint64_t k = grp[t];
       S.keys[t] = k;
       const int dxy = (int)(k & 3);
@@ -1067,25 +1180,25 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       spg += (int64_t)px * gx + (int64_t)py * gy;
     }
     Ext e;
-    e.min_x = block_reduce(mnx, MinOp(), S.red_u32);
-    e.max_x = block_reduce(mxx, MaxOp(), S.red_u32);
-    e.min_y = block_reduce(mny, MinOp(), S.red_u32);
-    e.max_y = block_reduce(mxy, MaxOp(), S.red_u32);
-    e.gx_sum = block_reduce(sgx, AddOp(), S.red_i32);
-    e.gy_sum = block_reduce(sgy, AddOp(), S.red_i32);
-    e.pg_sum = block_reduce(spg, AddOp(), S.red_i64);
+    e.min_x = team_reduce<NT>(mnx, MinOp(), S.red_u32);
+    e.max_x = team_reduce<NT>(mxx, MaxOp(), S.red_u32);
+    e.min_y = team_reduce<NT>(mny, MinOp(), S.red_u32);
+    e.max_y = team_reduce<NT>(mxy, MaxOp(), S.red_u32);
+    e.gx_sum = team_reduce<NT>(sgx, AddOp(), S.red_i32);
+    e.gy_sum = team_reduce<NT>(sgy, AddOp(), S.red_i32);
+    e.pg_sum = team_reduce<NT>(spg, AddOp(), S.red_i64);
     e.count = n;
     // ---- SelectBlobs (apriltag_gpu.cu:534-559); tag36h11: normal border only
     bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
     keep = keep && !((double)ext_dot(e) < 0.0);
-    if (!keep) continue;  // uniform across the workgroup
-    if (prm.diag_stop == 1) continue;
+    if (!keep) return;  // uniform across the workgroup
+    if (prm.diag_stop == 1) return;
     if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
     const uint32_t bi = rank & 0xfff;
 
     // ---- theta + sort key (P5/P6): (theta, plane, y, x) -----------------------
     const double cx = ext_cx(e), cy = ext_cy(e);
-    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+    for (uint32_t t = tid; t < n; t += NT) {
       const uint64_t k = S.keys[t];
       const int dxy = (int)(k & 3);
       const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
@@ -1101,17 +1214,17 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     }
     int np2 = 64;
     while (np2 < (int)n) np2 <<= 1;
-    for (int t = (int)n + tid; t < np2; t += kBlobThreads) S.keys[t] = ~0ull;
-    __syncthreads();
-    block_bitonic_sort<uint64_t, kBlobThreads>(S.keys, np2);
-    if (prm.diag_stop == 2) continue;
+    for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
+    team_sync<NT>();
+    team_bitonic_sort<uint64_t, NT>(S.keys, np2);
+    if (prm.diag_stop == 2) return;
 
     // ---- line-fit points + per-blob inclusive prefix sums (P7) -----------------
     {
       // Mx, My, W are int32 in the reference (LineFitPoint): wrap like two's complement
       uint32_t cMx = 0, cMy = 0, cW = 0;
       int64_t cMxx = 0, cMyy = 0, cMxy = 0;
-      for (uint32_t base = 0; base < n; base += kBlobThreads) {
+      for (uint32_t base = 0; base < n; base += NT) {
         const uint32_t t = base + tid;
         uint32_t vMx = 0, vMy = 0, vW = 0;
         int64_t vMxx = 0, vMyy = 0, vMxy = 0;
@@ -1132,12 +1245,12 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         }
         uint32_t tot;
         int64_t tot64;
-        const uint32_t pMx = block_incl_scan(vMx, S.red_u32, &tot) + cMx; cMx += tot;
-        const uint32_t pMy = block_incl_scan(vMy, S.red_u32, &tot) + cMy; cMy += tot;
-        const uint32_t pW = block_incl_scan(vW, S.red_u32, &tot) + cW; cW += tot;
-        const int64_t pMxx = block_incl_scan(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
-        const int64_t pMyy = block_incl_scan(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
-        const int64_t pMxy = block_incl_scan(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
+        const uint32_t pMx = team_incl_scan<NT>(vMx, S.red_u32, &tot) + cMx; cMx += tot;
+        const uint32_t pMy = team_incl_scan<NT>(vMy, S.red_u32, &tot) + cMy; cMy += tot;
+        const uint32_t pW = team_incl_scan<NT>(vW, S.red_u32, &tot) + cW; cW += tot;
+        const int64_t pMxx = team_incl_scan<NT>(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
+        const int64_t pMyy = team_incl_scan<NT>(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
+        const int64_t pMxy = team_incl_scan<NT>(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
         if (t < n) {
           P.Mx[t] = (int32_t)pMx; P.My[t] = (int32_t)pMy; P.W[t] = (int32_t)pW;
           P.Mxx[t] = pMxx; P.Myy[t] = pMyy; P.Mxy[t] = pMxy;
@@ -1149,11 +1262,11 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         }
       }
     }
-    __syncthreads();
-    if (prm.diag_stop == 3) continue;
+    team_sync<NT>();
+    if (prm.diag_stop == 3) return;
     // ---- errors, filter, peaks (K10 restated per blob, cyclic) ----------------
     const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
-    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+    for (uint32_t t = tid; t < n; t += NT) {
       const uint32_t i0 = (t + 2 * n - ksz) % n, i1 = (t + n + ksz) % n;
       const Moments m = read_moments(P, n, i0, i1);
       const int64_t Wl = m.W;
@@ -1164,8 +1277,8 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       const float eig = ((float)(Cxx + Cyy) - h) / (float)((double)(Wl * Wl) * 8.0);
       P.err[t] = (double)((float)m.N * eig);
     }
-    __syncthreads();
-    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+    team_sync<NT>();
+    for (uint32_t t = tid; t < n; t += NT) {
       double acc = 0.0;
 #pragma unroll
       for (int j = 0; j < 7; j++) {
@@ -1175,8 +1288,8 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       P.filt[t] = acc;
     }
     if (tid == 0) S.npeaks = 0;
-    __syncthreads();
-    for (uint32_t t = tid; t < n; t += kBlobThreads) {
+    team_sync<NT>();
+    for (uint32_t t = tid; t < n; t += NT) {
       const double me = P.filt[t];
       const double bef = P.filt[(t + n - 1) % n], aft = P.filt[(t + 1) % n];
       if (me > bef && me > aft) {
@@ -1187,16 +1300,16 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         S.keys[slot] = ((uint64_t)u << 32) | t;
       }
     }
-    __syncthreads();
+    team_sync<NT>();
     const uint32_t npk = S.npeaks;
     {
       int p2 = 2;
       while (p2 < (int)npk) p2 <<= 1;
-      for (int t = (int)npk + tid; t < p2; t += kBlobThreads) S.keys[t] = ~0ull;
-      __syncthreads();
-      if (npk > 1) block_bitonic_sort<uint64_t, kBlobThreads>(S.keys, p2);
+      for (int t = (int)npk + tid; t < p2; t += NT) S.keys[t] = ~0ull;
+      team_sync<NT>();
+      if (npk > 1) team_bitonic_sort<uint64_t, NT>(S.keys, p2);
     }
-    if (prm.diag_stop == 4) continue;
+    if (prm.diag_stop == 4) return;
     // ---- FitQuads (K11) --------------------------------------------------------
     const int cnt = (int)npk;
     if (tid < 16) {
@@ -1209,9 +1322,9 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       }
       S.pi[r] = v;
     }
-    __syncthreads();
-    if (cnt >= 4 && tid < 28) {
-      const int m0 = c_m0m1[tid][0], m1 = c_m0m1[tid][1];
+    team_sync<NT>();
+    for (int c = tid; cnt >= 4 && c < 28; c += NT) {
+      const int m0 = c_m0m1[c][0], m1 = c_m0m1[c][1];
       if (m1 < kNMaxima && m1 < cnt) {
         const LineFitOut o = fit_line_v<false, true>(read_moments(P, n, S.pi[m0], S.pi[m1]));
         S.e01[m0][m1 - 1] = o.mse > (double)prm.max_line_fit_mse ? DBL_MAX : o.err;
@@ -1221,43 +1334,49 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         S.e01[m0][m1 - 1] = DBL_MAX;
       }
     }
-    __syncthreads();
-    if (prm.diag_stop == 7) continue;
+    team_sync<NT>();
+    if (prm.diag_stop == 7) return;
+    // 210 lexicographic combinations; each lane keeps its first minimum
     double err = DBL_MAX;
-    if (tid < 210 && cnt >= 4) {
-      const int m0 = c_combo[tid][0], m1 = c_combo[tid][1], m2 = c_combo[tid][2], m3 = c_combo[tid][3];
-      const double e01 = S.e01[m0][m1 - 1];
-      if (m3 < cnt && e01 != DBL_MAX) {
-        const LineFitOut o12 = fit_line_v<false, true>(read_moments(P, n, S.pi[m1], S.pi[m2]));
-        if (!(o12.mse > (double)prm.max_line_fit_mse)) {
-          const double dot = S.lp01[m0][m1 - 1][0] * o12.p23[0] + S.lp01[m0][m1 - 1][1] * o12.p23[1];
-          if (!(fabs(dot) > prm.cos_critical_rad)) {
-            const LineFitOut o23 = fit_line_v<false, false>(read_moments(P, n, S.pi[m2], S.pi[m3]));
-            if (!(o23.mse > (double)prm.max_line_fit_mse)) {
-              const LineFitOut o30 = fit_line_v<false, false>(read_moments(P, n, S.pi[m3], S.pi[m0]));
-              if (!(o30.mse > (double)prm.max_line_fit_mse)) err = e01 + o12.err + o23.err + o30.err;
+    uint32_t bt = 0xffffffffu;
+    for (int c = tid; c < 210; c += NT) {
+      double e4 = DBL_MAX;
+      if (cnt >= 4) {
+        const int m0 = c_combo[c][0], m1 = c_combo[c][1], m2 = c_combo[c][2], m3 = c_combo[c][3];
+        const double e01 = S.e01[m0][m1 - 1];
+        if (m3 < cnt && e01 != DBL_MAX) {
+          const LineFitOut o12 = fit_line_v<false, true>(read_moments(P, n, S.pi[m1], S.pi[m2]));
+          if (!(o12.mse > (double)prm.max_line_fit_mse)) {
+            const double dot = S.lp01[m0][m1 - 1][0] * o12.p23[0] + S.lp01[m0][m1 - 1][1] * o12.p23[1];
+            if (!(fabs(dot) > prm.cos_critical_rad)) {
+              const LineFitOut o23 = fit_line_v<false, false>(read_moments(P, n, S.pi[m2], S.pi[m3]));
+              if (!(o23.mse > (double)prm.max_line_fit_mse)) {
+                const LineFitOut o30 = fit_line_v<false, false>(read_moments(P, n, S.pi[m3], S.pi[m0]));
+                if (!(o30.mse > (double)prm.max_line_fit_mse)) e4 = e01 + o12.err + o23.err + o30.err;
+              }
             }
           }
         }
       }
+      if (bt == 0xffffffffu || e4 < err) { err = e4; bt = (uint32_t)c; }
     }
     // BlockReduce(MinQuadError): minimum error, first (lowest) combination on ties
-    {
-      uint32_t bt = tid < 210 ? (uint32_t)tid : 0xffffffffu;
 #pragma unroll
-      for (int d = 32; d > 0; d >>= 1) {
-        const double oe = __shfl_xor(err, d);
-        const uint32_t ot = __shfl_xor(bt, d);
-        if (oe < err || (oe == err && ot < bt)) { err = oe; bt = ot; }
-      }
-      if (lane == 0) { S.red_f64[tid >> 6] = err; S.red_idx[tid >> 6] = bt; }
+    for (int d = 32; d > 0; d >>= 1) {
+      const double oe = __shfl_xor(err, d);
+      const uint32_t ot = __shfl_xor(bt, d);
+      if (oe < err || (oe == err && ot < bt)) { err = oe; bt = ot; }
     }
-    __syncthreads();
-    if (prm.diag_stop == 8) continue;
-    double best = S.red_f64[0];
-    uint32_t bt = S.red_idx[0];
-    for (int i = 1; i < kBlobThreads / 64; i++)
-      if (S.red_f64[i] < best || (S.red_f64[i] == best && S.red_idx[i] < bt)) { best = S.red_f64[i]; bt = S.red_idx[i]; }
+    if constexpr (NT > 64) {
+      if (lane == 0) { S.red_f64[tid >> 6] = err; S.red_idx[tid >> 6] = bt; }
+      team_sync<NT>();
+      err = S.red_f64[0];
+      bt = S.red_idx[0];
+      for (int i = 1; i < NT / 64; i++)
+        if (S.red_f64[i] < err || (S.red_f64[i] == err && S.red_idx[i] < bt)) { err = S.red_f64[i]; bt = S.red_idx[i]; }
+    }
+    if (prm.diag_stop == 8) return;
+    double best = err;
     if (bt >= 210) bt = 0;
     const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
     uint16_t qidx[4];
@@ -1270,7 +1389,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
       S.lines[tid][2] = o.p23[0];
       S.lines[tid][3] = o.p23[1];
     }
-    __syncthreads();
+    team_sync<NT>();
     if (tid == 0) {
       QuadRecord rec;
       rec.blob_index = bi;
@@ -1333,7 +1452,56 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
         else atomicOr(b.status + f, kStatusQuadsOverflow);
       }
     }
+  team_sync<NT>();
+}
+
+__device__ __forceinline__ BlobScratch blob_scratch(const DevBufs& b, size_t team, int cap) {
+  BlobScratch P;
+  P.Mx = b.s_i32 + (team * 3 + 0) * cap;
+  P.My = b.s_i32 + (team * 3 + 1) * cap;
+  P.W = b.s_i32 + (team * 3 + 2) * cap;
+  P.Mxx = b.s_i64 + (team * 3 + 0) * cap;
+  P.Myy = b.s_i64 + (team * 3 + 1) * cap;
+  P.Mxy = b.s_i64 + (team * 3 + 2) * cap;
+  P.err = b.s_f64 + (team * 2 + 0) * cap;
+  P.filt = b.s_f64 + (team * 2 + 1) * cap;
+  return P;
+}
+
+// K9a (large blobs, > kSmallBlob points): one blob per 256-thread workgroup
+// iteration, persistent over the large work list.
+__global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params prm) {
+  __shared__ BlobShared<kSortCap> S;
+  const int tid = threadIdx.x;
+  const BlobScratch P = blob_scratch(b, blockIdx.x, kSortCap);
+  if (tid == 0) S.nwork = *b.nwork;
+  __syncthreads();
+  const uint32_t nwork = S.nwork;
+  while (true) {
+    if (tid == 0) S.item = atomicAdd(b.workhead, 1u);
     __syncthreads();
+    const uint32_t item = S.item;
+    __syncthreads();
+    if (item >= nwork) break;
+    blob_item<kBlobThreads, kSortCap>(b, g, prm, S, P, b.work[item]);
+  }
+}
+
+// K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
+// waves per workgroup, persistent over the small work list.
+__global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params prm) {
+  __shared__ BlobShared<kSmallBlob> Ss[4];
+  const int wave = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  BlobShared<kSmallBlob>& S = Ss[wave];
+  const BlobScratch P = blob_scratch(b, (size_t)blockIdx.x * 4 + wave, kSmallBlob);
+  const uint32_t nwork = *b.nwork_small;
+  while (true) {
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(b.workhead_small, 1u);
+    item = __shfl(item, 0);
+    if (item >= nwork) break;
+    blob_item<64, kSmallBlob>(b, g, prm, S, P, b.work_small[item]);
   }
 }
 
@@ -1678,13 +1846,15 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     mark();
   }
   {
-    dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 3) / 4, B);
+    dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows), B);
     hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
     mark();
   }
-  hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g);
+  hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
   mark();
   hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
+  mark();
+  hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st, b, g, prm);
   mark();
   hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
   mark();

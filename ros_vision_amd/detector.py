@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(_HERE, "libat_hip.so")
 
 AT_FMT_YUYV, AT_FMT_BGR8, AT_FMT_GRAY8 = 0, 1, 2
 (AT_STAGE_GRAY, AT_STAGE_DECIMATED, AT_STAGE_THRESHOLD, AT_STAGE_LABELS, AT_STAGE_SIZES,
- AT_STAGE_NUM_POINTS, AT_STAGE_NUM_PAIRS, AT_STAGE_QUADS, AT_STAGE_POINTS, AT_STAGE_BLOB_POINTS) = range(10)
+ AT_STAGE_NUM_POINTS, AT_STAGE_NUM_PAIRS, AT_STAGE_QUADS, AT_STAGE_POINTS, AT_STAGE_BLOB_POINTS,
+ AT_STAGE_NUM_PAIR_ENTRIES, AT_STAGE_PROBE) = range(12)
 AT_E_CAPACITY = -3
 
 # Symbols declared in include/at_api.h (checked by tests/test_abi.py).
@@ -298,6 +299,14 @@ class GpuDetector:
 
     def num_pairs(self, frame=0):
         return int(self._copy(AT_STAGE_NUM_PAIRS, frame, 4, np.uint32)[0])
+
+    def num_pair_entries(self, frame=0):
+        """Per-tile pair-histogram entries k_boundary handed to k_pairs (diagnostic)."""
+        return int(self._copy(AT_STAGE_NUM_PAIR_ENTRIES, frame, 4, np.uint32)[0])
+
+    def copy_probe(self):
+        """Kernel phase clock stamps (100 MHz wall clock) written when AT_PHASE_PROBE is set."""
+        return self._copy(AT_STAGE_PROBE, 0, 8 * 256, np.uint64)
 
     def copy_points(self, frame=0):
         """Boundary points (QuadBoundaryPoint keys), device emission order."""
