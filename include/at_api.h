@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define AT_ABI_VERSION 1
+#define AT_ABI_VERSION 2
 
 enum {
   AT_OK = 0,
@@ -60,6 +60,9 @@ typedef struct {
   double cos_critical_rad;    /* cos(10 deg) */
   int device;                 /* HIP device ordinal */
   int max_batch;              /* frames per at_detect_batch / at_detect_device call */
+  double tag_size;            /* metres; > 0 also estimates every tag's pose on the GPU
+                                 (info_.tagsize = TAGSIZE 0.1651, apriltags_cuda_detector.cu:185,
+                                 apriltags_cuda_detector.hpp:39); 0 = detection only */
 } at_config;
 
 /* apriltag_detection_t fields published downstream (apriltag.h; consumed at
@@ -141,6 +144,34 @@ typedef struct {
 int at_set_profiling(at_detector *d, int enable);
 int at_stage_times(at_detector *d, double *ms, int cap);
 const char *at_stage_name(int stage);
+
+/* Tag pose of each detection of the last collected batch (row A23): the
+ * reference node's estimate_tag_pose(&info_, &pose) per detection
+ * (apriltags_cuda_detector.cu:425-436; AprilTag 3.x orthogonal iteration with
+ * the second-minimum check), computed on the GPU by the k_pose kernel when
+ * at_config.tag_size > 0.  Entry i belongs to detection i of the frame (the
+ * id-sorted order at_collect returned).  Returns the count or < 0. */
+typedef struct {
+  int32_t id;
+  double R[9];     /* row-major rotation, tag -> camera */
+  double t[3];     /* tag centre in the camera frame, metres (pose.t) */
+  double err;      /* object-space error returned by estimate_tag_pose */
+} at_pose;
+int at_poses(at_detector *d, int frame, at_pose *out, int cap);
+
+/* The node's per-frame tail over those poses (apriltags_cuda_detector.cu:425-462,
+ * 595-599): robot = R_ext * t + t_ext (transformCameraToRobot), distance = |t|
+ * in the camera frame, records sorted by ascending distance (stable).  Host
+ * only; extr_R row-major 3x3 (NULL = identity), extr_t 3 (NULL = zero). */
+typedef struct {
+  int32_t id;
+  double camera[3];   /* aprilTagInCameraFrame */
+  double robot[3];    /* aprilTagInRobotFrame */
+  double distance;
+  double err;         /* pose_error */
+} at_tag_detection;
+int at_tag_detections(const at_pose *poses, int n, const double *extr_R, const double *extr_t,
+                      at_tag_detection *out);
 
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);

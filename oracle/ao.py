@@ -80,6 +80,9 @@ def lib():
             getattr(L, n).restype = C.c_float
             getattr(L, n).argtypes = [C.c_float]
         L.ao_rotate90.restype = C.c_uint64
+        D = C.POINTER(C.c_double)
+        L.ao_estimate_tag_pose.argtypes = [D, D, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                           D, D, D]
         L.ao_rotate90.argtypes = [C.c_uint64]
         L.ao_unrank.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
         _LIB = L
@@ -180,6 +183,20 @@ class Oracle:
 
     def status(self):
         return lib().ao_status(self.h)
+
+
+def estimate_tag_pose(H, corners, fx, fy, cx, cy, tagsize=0.1651):
+    """estimate_tag_pose restatement (ao_pose.c): returns (R 3x3, t 3, err, (err1, err2), second_won)."""
+    D = C.POINTER(C.c_double)
+    H = np.ascontiguousarray(H, np.float64).reshape(9)
+    P = np.ascontiguousarray(corners, np.float64).reshape(8)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    e = np.zeros(2)
+    sec = lib().ao_estimate_tag_pose(H.ctypes.data_as(D), P.ctypes.data_as(D), fx, fy, cx, cy, tagsize,
+                                     R.ctypes.data_as(D), t.ctypes.data_as(D), e.ctypes.data_as(D))
+    err = e[0] if e[0] <= e[1] else e[1]
+    return R.reshape(3, 3), t, err, (e[0], e[1]), bool(sec)
 
 
 def family_entries():

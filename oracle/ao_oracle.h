@@ -110,6 +110,13 @@ float ao_det_cosf(float x);
 float ao_det_sinf(float x);
 float ao_det_hypotf(float a, float b);
 
+/* tag pose (ao_pose.c; estimate_tag_pose of the un-vendored AprilTag 3.x library,
+ * called at apriltags_cuda_detector.cu:433).  R row-major, t in metres,
+ * err = {err1, err2} object-space errors of the two minima (err2 = HUGE_VAL when
+ * there is no second minimum).  Returns 1 when the second solution won. */
+int ao_estimate_tag_pose(const double H[9], const double corners[4][2], double fx, double fy, double cx, double cy,
+                         double tagsize, double R[9], double t[3], double err[2]);
+
 /* helpers exposed for tests */
 uint64_t ao_rotate90(uint64_t w);
 int ao_unrank(int i, int *m0, int *m1, int *m2, int *m3);

@@ -4,8 +4,10 @@ Product code: HIP kernels + C ABI in ``csrc/`` (built into ``libat_hip.so``),
 the Python mirror of the reference GpuDetector interface in ``detector.py``
 and the synthetic tag-board generator in ``synth.py``.
 """
-from .detector import (AT_FMT_BGR8, AT_FMT_GRAY8, AT_FMT_YUYV, CameraMatrix, Detection,  # noqa: F401
-                       DistCoeffs, GpuDetector, family_entries, load_library)
+from .detector import (AT_FMT_BGR8, AT_FMT_GRAY8, AT_FMT_YUYV, TAG_SIZE, TEST_CAMERA, TEST_DIST,  # noqa: F401
+                       CameraMatrix, Detection, DistCoeffs, GpuDetector, Pose, TagDetection, family_entries,
+                       load_library, tag_detections)
 
-__all__ = ["GpuDetector", "CameraMatrix", "DistCoeffs", "Detection", "load_library", "family_entries",
+__all__ = ["GpuDetector", "CameraMatrix", "DistCoeffs", "Detection", "Pose", "TagDetection", "load_library",
+           "family_entries", "tag_detections", "TAG_SIZE", "TEST_CAMERA", "TEST_DIST",
            "AT_FMT_YUYV", "AT_FMT_BGR8", "AT_FMT_GRAY8"]

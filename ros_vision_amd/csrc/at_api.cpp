@@ -54,6 +54,8 @@ struct at_detector {
   size_t ctrl_words;
   uint32_t* h_ctrl;         // pinned copy of the control block
   DevDetection* h_dets;     // pinned [B][kMaxDets]
+  std::vector<at_pose> poses;   // [B][kMaxDets] poses of the last collected batch (id order)
+  std::vector<int> nposes;      // [B]
   int last_nframes;
   int pending;
   hipEvent_t ev_done;
@@ -121,6 +123,7 @@ int at_config_default(at_config* cfg, int width, int height) {
   cfg->cos_critical_rad = cos(10.0 * M_PI / 180.0);
   cfg->device = 0;
   cfg->max_batch = 1;
+  cfg->tag_size = 0.1651;  // TAGSIZE, apriltags_cuda_detector.hpp:39
   return AT_OK;
 }
 
@@ -176,6 +179,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
+  if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) return AT_E_INVALID;
+  p.tag_size = cfg->tag_size;
 
   auto fail = [&](int code) {
     at_destroy(d);
@@ -252,6 +257,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.s_f64 = (double*)dalloc(nw * 2 * 8);
   if (oom) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
+  d->poses.assign(B * kMaxDets, at_pose{});
+  d->nposes.assign(B, 0);
   if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_dets, B * kMaxDets * sizeof(DevDetection), hipHostMallocDefault) != hipSuccess)
     return fail(AT_E_NOMEM);
@@ -308,7 +315,7 @@ static int prefer_smaller(int pref, double q0, double q1) {
   return 0;
 }
 
-static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int cap) {
+static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int cap, at_pose* poses) {
   std::vector<DevDetection> v(cand, cand + ncand);
   std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.blob_rank < b.blob_rank; });
   int n = (int)v.size();
@@ -334,6 +341,12 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
   }
   v.resize(n);
   std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.id < b.id; });
+  for (int i = 0; i < n && i < kMaxDets; i++) {
+    poses[i].id = v[i].id;
+    memcpy(poses[i].R, v[i].pose_R, sizeof(poses[i].R));
+    memcpy(poses[i].t, v[i].pose_t, sizeof(poses[i].t));
+    poses[i].err = v[i].pose_err[0] <= v[i].pose_err[1] ? v[i].pose_err[0] : v[i].pose_err[1];  // estimate_tag_pose
+  }
   for (int i = 0; i < n && i < cap; i++) {
     at_detection& o = out[i];
     o.id = v[i].id;
@@ -382,8 +395,9 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
       rc = AT_E_CAPACITY;
     } else {
       n = host_tail(d->h_dets + (size_t)f * kMaxDets, ncand, out ? out + (size_t)f * cap_per_frame : nullptr,
-                    out ? cap_per_frame : 0);
+                    out ? cap_per_frame : 0, d->poses.data() + (size_t)f * kMaxDets);
     }
+    d->nposes[f] = d->prm.tag_size > 0 ? std::min(n, kMaxDets) : 0;
     if (n_per_frame) n_per_frame[f] = n;
   }
   return rc;
@@ -463,6 +477,36 @@ int at_stage_times(at_detector* d, double* ms, int cap) {
 
 const char* at_stage_name(int stage) {
   return (stage >= 0 && stage < kNumStages) ? kStageNames[stage] : "";
+}
+
+int at_poses(at_detector* d, int frame, at_pose* out, int cap) {
+  if (!d || frame < 0 || frame >= d->last_nframes || (cap > 0 && !out)) return AT_E_INVALID;
+  if (d->pending) return AT_E_INVALID;  // collect first
+  const int n = d->nposes[frame];
+  for (int i = 0; i < n && i < cap; i++) out[i] = d->poses[(size_t)frame * kMaxDets + i];
+  return n;
+}
+
+int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const double* extr_t,
+                      at_tag_detection* out) {
+  if (n < 0 || (n > 0 && (!poses || !out))) return AT_E_INVALID;
+  static const double kEye[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, kZero[3] = {0, 0, 0};
+  const double* Re = extr_R ? extr_R : kEye;
+  const double* te = extr_t ? extr_t : kZero;
+  std::vector<at_tag_detection> v((size_t)n);
+  for (int i = 0; i < n; i++) {
+    at_tag_detection& o = v[i];
+    o.id = poses[i].id;
+    for (int k = 0; k < 3; k++) o.camera[k] = poses[i].t[k];
+    for (int r = 0; r < 3; r++)  // extrinsic_rotation_ * camera_point_mat + extrinsic_offset_
+      o.robot[r] = Re[r * 3 + 0] * o.camera[0] + Re[r * 3 + 1] * o.camera[1] + Re[r * 3 + 2] * o.camera[2] + te[r];
+    o.distance = std::sqrt(o.camera[0] * o.camera[0] + o.camera[1] * o.camera[1] + o.camera[2] * o.camera[2]);
+    o.err = poses[i].err;
+  }
+  std::stable_sort(v.begin(), v.end(),
+                   [](const at_tag_detection& a, const at_tag_detection& b) { return a.distance < b.distance; });
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return n;
 }
 
 int at_frame_status(at_detector* d, int frame) {

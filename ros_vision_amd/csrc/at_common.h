@@ -21,9 +21,10 @@ constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wa
 constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
-constexpr int kNumStages = 10;
+constexpr int kNumStages = 11;
 constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final", "k_boundary",
-                                                 "k_pairs", "k_group",   "k_blob_small", "k_blob",       "k_decode"};
+                                                 "k_pairs", "k_group",   "k_blob_small", "k_blob",       "k_decode",
+                                                 "k_pose"};
 
 // ---- per-frame status bits -------------------------------------------------
 constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs
@@ -53,6 +54,7 @@ struct Params {
   int refine_edges;
   double fx, fy, cx, cy, k1, k2, p1, p2, k3;
   int diag_stop;  // diagnostics only (AT_DIAG_BLOB_STOP): k_blob returns after phase N; 0 = full
+  double tag_size;  // metres; > 0 runs k_pose (apriltags_cuda_detector.hpp:39 TAGSIZE)
   int probe;      // diagnostics only (AT_PHASE_PROBE): kernels stamp phase clocks into DevBufs::probe
 };
 constexpr int kProbeWords = 256;
@@ -65,6 +67,10 @@ struct DevDetection {
   double H[9];
   double c[2];
   double p[4][2];
+  // estimate_tag_pose (k_pose, when Params::tag_size > 0)
+  double pose_R[9];
+  double pose_t[3];
+  double pose_err[2];  // errors of the first / second minimum (HUGE_VAL: none)
 };
 
 // Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode.

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "at_common.h"
+#include "at_pose.h"
 
 namespace at {
 
@@ -1156,6 +1157,16 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
                           const BlobScratch& P, uint32_t w) {
   const int tid = team_rank<NT>();
   const uint32_t lane = lane_id();
+  // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k])
+  uint64_t t_last = prm.probe ? wall_clock64() : 0;
+  auto phase = [&](int k) {
+    if (prm.probe && tid == 0) {
+      const uint64_t now = wall_clock64();
+      atomicAdd((unsigned long long*)&b.probe[64 + (NT > 64 ? 16 : 0) + k], (unsigned long long)(now - t_last));
+      atomicAdd((unsigned long long*)&b.probe[96 + (NT > 64 ? 16 : 0) + k], 1ull);
+      t_last = now;
+    }
+  };
     const int f = (int)(w >> 16);
     const uint32_t rank = w & 0xffff;
     const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
@@ -1191,7 +1202,9 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     // ---- SelectBlobs (apriltag_gpu.cu:534-559); tag36h11: normal border only
     bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
     keep = keep && !((double)ext_dot(e) < 0.0);
+    phase(0);
     if (!keep) return;  // uniform across the workgroup
+    phase(1);
     if (prm.diag_stop == 1) return;
     if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
     const uint32_t bi = rank & 0xfff;
@@ -1217,6 +1230,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
     team_sync<NT>();
     team_bitonic_sort<uint64_t, NT>(S.keys, np2);
+    phase(2);
     if (prm.diag_stop == 2) return;
 
     // ---- line-fit points + per-blob inclusive prefix sums (P7) -----------------
@@ -1263,6 +1277,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       }
     }
     team_sync<NT>();
+    phase(3);
     if (prm.diag_stop == 3) return;
     // ---- errors, filter, peaks (K10 restated per blob, cyclic) ----------------
     const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
@@ -1309,6 +1324,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       team_sync<NT>();
       if (npk > 1) team_bitonic_sort<uint64_t, NT>(S.keys, p2);
     }
+    phase(4);
     if (prm.diag_stop == 4) return;
     // ---- FitQuads (K11) --------------------------------------------------------
     const int cnt = (int)npk;
@@ -1335,6 +1351,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       }
     }
     team_sync<NT>();
+    phase(7);
     if (prm.diag_stop == 7) return;
     // 210 lexicographic combinations; each lane keeps its first minimum
     double err = DBL_MAX;
@@ -1375,6 +1392,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       for (int i = 1; i < NT / 64; i++)
         if (S.red_f64[i] < err || (S.red_f64[i] == err && S.red_idx[i] < bt)) { err = S.red_f64[i]; bt = S.red_idx[i]; }
     }
+    phase(8);
     if (prm.diag_stop == 8) return;
     double best = err;
     if (bt >= 210) bt = 0;
@@ -1452,6 +1470,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
         else atomicOr(b.status + f, kStatusQuadsOverflow);
       }
     }
+  phase(9);
   team_sync<NT>();
 }
 
@@ -1819,6 +1838,20 @@ hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
 
 // Kernel order of one launch sequence; ev (optional, kNumStages+1 events)
 // brackets every kernel for per-stage timing.
+// ---------------------------------------------------------------------------
+// K11: tag pose of every decoded candidate (row A23: estimate_tag_pose at
+// apriltags_cuda_detector.cu:433), one thread per detection.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
+  const int f = blockIdx.y;
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
+  if (i >= n) return;
+  DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
+  pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, d.pose_R, d.pose_t, d.pose_err,
+                          (prm.probe && f == 0 && i == 0) ? b.probe + 16 : nullptr);
+}
+
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev) {
   int e = 0;
@@ -1859,6 +1892,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
   mark();
   hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm);
+  mark();
+  if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
   mark();
   return hipGetLastError();
 }

@@ -29,8 +29,10 @@ EXPORTS = [
     "at_config_default", "at_create", "at_detect", "at_detect_batch", "at_detect_device",
     "at_enqueue_device", "at_collect", "at_frame_status", "at_debug_copy", "at_destroy",
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
-    "at_set_profiling", "at_stage_times", "at_stage_name",
+    "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
 ]
+
+TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
 
 
 class AtConfig(C.Structure):
@@ -39,7 +41,7 @@ class AtConfig(C.Structure):
         ("quad_decimate", C.c_float), ("refine_edges", C.c_int), ("decode_sharpening", C.c_double),
         ("min_white_black_diff", C.c_int), ("min_cluster_pixels", C.c_int), ("max_nmaxima", C.c_int),
         ("max_line_fit_mse", C.c_float), ("cos_critical_rad", C.c_double),
-        ("device", C.c_int), ("max_batch", C.c_int),
+        ("device", C.c_int), ("max_batch", C.c_int), ("tag_size", C.c_double),
     ]
 
 
@@ -52,6 +54,15 @@ class AtDetection(C.Structure):
         ("id", C.c_int32), ("hamming", C.c_int32), ("decision_margin", C.c_float),
         ("H", C.c_double * 9), ("c", C.c_double * 2), ("p", (C.c_double * 2) * 4),
     ]
+
+
+class AtPose(C.Structure):
+    _fields_ = [("id", C.c_int32), ("R", C.c_double * 9), ("t", C.c_double * 3), ("err", C.c_double)]
+
+
+class AtTagDetection(C.Structure):
+    _fields_ = [("id", C.c_int32), ("camera", C.c_double * 3), ("robot", C.c_double * 3),
+                ("distance", C.c_double), ("err", C.c_double)]
 
 
 class AtQuadRecord(C.Structure):
@@ -70,6 +81,26 @@ class Detection:
     H: np.ndarray
     c: np.ndarray
     p: np.ndarray
+
+
+@dataclass
+class Pose:
+    """apriltag_pose_t + the error estimate_tag_pose returns (apriltags_cuda_detector.cu:432-433)."""
+    id: int
+    R: np.ndarray
+    t: np.ndarray
+    err: float
+
+
+@dataclass
+class TagDetection:
+    """DetectionData of the node loop (apriltags_cuda_detector.cu:425-462): camera- and
+    robot-frame position, distance from the camera, pose error."""
+    id: int
+    camera: np.ndarray
+    robot: np.ndarray
+    distance: float
+    err: float
 
 
 @dataclass
@@ -136,6 +167,9 @@ def load_library(path: str = LIB_PATH):
     L.at_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
     L.at_stage_name.restype = C.c_char_p
     L.at_stage_name.argtypes = [C.c_int]
+    L.at_poses.argtypes = [C.c_void_p, C.c_int, C.POINTER(AtPose), C.c_int]
+    L.at_tag_detections.argtypes = [C.POINTER(AtPose), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                    C.POINTER(AtTagDetection)]
     _LIB = L
     return L
 
@@ -150,6 +184,31 @@ def family_entries(family: str = "tag36h11"):
         L.at_family_entry(family.encode(), i, C.byref(tid), C.byref(code))
         out.append((tid.value, code.value))
     return out
+
+
+def tag_detections(poses, extrinsic_rotation=None, extrinsic_offset=None):
+    """The node's per-frame tail (apriltags_cuda_detector.cu:425-462, 595-599):
+    transformCameraToRobot + distance, sorted closest first.  Runs in libat_hip.so
+    (host code, no device needed)."""
+    L = load_library()
+    n = len(poses)
+    arr = (AtPose * max(1, n))()
+    for i, p in enumerate(poses):
+        arr[i].id = int(p.id)
+        arr[i].R[:] = [float(x) for x in np.asarray(p.R, np.float64).ravel()]
+        arr[i].t[:] = [float(x) for x in np.asarray(p.t, np.float64).ravel()]
+        arr[i].err = float(p.err)
+    Rp = tp = None
+    if extrinsic_rotation is not None:
+        Rv = np.ascontiguousarray(extrinsic_rotation, np.float64).reshape(9)
+        Rp = Rv.ctypes.data_as(C.POINTER(C.c_double))
+    if extrinsic_offset is not None:
+        tv = np.ascontiguousarray(extrinsic_offset, np.float64).reshape(3)
+        tp = tv.ctypes.data_as(C.POINTER(C.c_double))
+    out = (AtTagDetection * max(1, n))()
+    _check(L.at_tag_detections(arr, n, Rp, tp, out), "at_tag_detections")
+    return [TagDetection(id=o.id, camera=np.array(list(o.camera)), robot=np.array(list(o.robot)),
+                         distance=o.distance, err=o.err) for o in out[:n]]
 
 
 def _check(rc, what):
@@ -242,6 +301,14 @@ class GpuDetector:
         _check(load_library().at_enqueue_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt),
                "at_enqueue_device")
         self._pending = nframes
+
+    def poses(self, frame=0):
+        """Pose of each detection of `frame` of the last batch (same order as its
+        detections), computed on the GPU (k_pose) when tag_size > 0."""
+        buf = (AtPose * self._cap)()
+        n = _check(load_library().at_poses(self._h, frame, buf, self._cap), "at_poses")
+        return [Pose(id=b.id, R=np.array(list(b.R)).reshape(3, 3), t=np.array(list(b.t)), err=b.err)
+                for b in buf[:min(n, self._cap)]]
 
     def collect(self):
         rc = load_library().at_collect(self._h, self._out, self._cap, self._n)

@@ -157,3 +157,54 @@ def test_gpu_matches_committed_golden(gpu, name):
         assert np.allclose(a.p, np.array(b["p"]), atol=1e-4) and np.allclose(a.c, np.array(b["c"]), atol=1e-4)
         assert np.allclose(a.H.ravel(), np.array(b["H"]), atol=1e-4)
         assert np.array_equal(np.floor(a.p), np.floor(np.array(b["p"])))
+
+
+# ---- row A23: tag pose (k_pose) against the oracle's estimate_tag_pose -------
+
+def _pose_close(a_R, a_t, b_R, b_t, tol):
+    return np.abs(np.asarray(a_R) - np.asarray(b_R)).max() <= tol and np.abs(np.asarray(a_t) - np.asarray(b_t)).max() <= tol
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+def test_pose_parity_720p(gpu, oracle_mod, frame):
+    """GPU pose of every detection vs the oracle pose of the oracle's detection
+    with the same id: within 1e-4 (north star float tolerance)."""
+    from ros_vision_amd import synth
+    cam = gpu.TEST_CAMERA
+    yuyv, _, _ = synth.stream_frame(1280, 720, frame)
+    det = gpu.GpuDetector(1280, 720)
+    dets = det.detect(yuyv)
+    poses = det.poses()
+    assert len(poses) == len(dets) > 0
+    orc = oracle_mod.Oracle(1280, 720)
+    orc.detect(yuyv, 0)
+    odets = {d["id"]: d for d in orc.detections()}
+    worst = 0.0
+    for d, p in zip(dets, poses):
+        assert p.id == d.id
+        od = odets[d.id]
+        R, t, err, (e1, e2), _ = oracle_mod.estimate_tag_pose(od["H"], od["p"], cam.fx, cam.fy, cam.cx, cam.cy)
+        if abs(e1 - e2) <= 1e-9 * max(e1, e2, 1e-30):
+            continue  # two minima with equal error: either is the reference's answer
+        worst = max(worst, np.abs(p.R - R).max(), np.abs(p.t - t).max())
+        assert _pose_close(p.R, p.t, R, t, 1e-4), (d.id, p.R, R, p.t, t)
+        assert abs(p.err - err) <= 1e-4 * max(1.0, abs(err))
+    # same inputs (the GPU's own H and corners) agree far tighter
+    for d, p in zip(dets, poses):
+        R, t, _, _, _ = oracle_mod.estimate_tag_pose(d.H, d.p, cam.fx, cam.fy, cam.cx, cam.cy)
+        assert _pose_close(p.R, p.t, R, t, 1e-9), d.id
+    print("pose worst |diff| vs oracle detections: %.3g" % worst)
+
+
+def test_pose_disabled_and_camera_to_robot(gpu):
+    from ros_vision_amd import synth
+    yuyv, _, _ = synth.stream_frame(1280, 720, 0)
+    off = gpu.GpuDetector(1280, 720, tag_size=0.0)
+    assert len(off.detect(yuyv)) > 0 and off.poses() == []
+    on = gpu.GpuDetector(1280, 720)
+    on.detect(yuyv)
+    tags = gpu.tag_detections(on.poses(), np.eye(3), np.zeros(3))
+    d = [t.distance for t in tags]
+    assert d == sorted(d) and len(tags) == len(on.poses())
+    for t in tags:
+        assert np.allclose(t.camera, t.robot) and t.camera[2] > 0
