@@ -14,10 +14,15 @@
 //     column (tag corners lie in z = 0), so U V' restricted to the first two
 //     columns is the polar factor of the 3x2 block A (A'A)^-1/2 (2x2 closed
 //     form), and the det(R) < 0 column-2 flip leaves column 2 = c0 x c1.
-// One thread per detection; everything in double.
+// One thread per detection; everything in double.  The k_pose chain is
+// latency-bound (one wave per 64 tags), so FMA contraction is allowed here
+// (float tolerance 1e-4, unlike the bit-exact integer stages) and the
+// per-step sums are balanced trees.
 #pragma once
 
 #include "at_detmath.h"
+
+#pragma clang fp contract(fast)
 
 namespace at {
 namespace pose {
@@ -140,8 +145,8 @@ __device__ M3 polar_rank2_proper(const M3& m) {
   const double tau = sqrt(a + c + 2 * d);
   // (S + d I)^-1 * tau
   const double e00 = a + d, e01 = b, e11 = c + d;
-  const double edet = e00 * e11 - e01 * e01;
-  const double i00 = tau * e11 / edet, i01 = -tau * e01 / edet, i11 = tau * e00 / edet;
+  const double k = tau / (e00 * e11 - e01 * e01);
+  const double i00 = e11 * k, i01 = -e01 * k, i11 = e00 * k;
   M3 r;
   V3 q0, q1;
 #pragma unroll
@@ -181,7 +186,7 @@ __device__ __forceinline__ M3 calculate_F(const V3& v) {
 // (fixed point or 2-cycle) the remaining steps are known exactly and the loop
 // stops.  As upstream, the returned t belongs to the R before the last step
 // and the error to the final (R, t).
-__device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, int n_steps) {
+__device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, int n_steps, int* steps = nullptr) {
   M3 F[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) F[k] = calculate_F(v[k]);
@@ -238,7 +243,14 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
   bool cyc2 = false;
   for (k = 1; k <= n_steps; k++) {
     M3 M;
-    const V3 m0 = v_add(mv(A00, r0), mv(A01, r1)), m1 = v_add(mv(A10, r0), mv(A11, r1));
+    V3 m0, m1;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {  // balanced 6-term dot products
+      m0.v[i] = ((A00.m[i][0] * r0.v[0] + A00.m[i][1] * r0.v[1]) + (A00.m[i][2] * r0.v[2] + A01.m[i][0] * r1.v[0])) +
+                (A01.m[i][1] * r1.v[1] + A01.m[i][2] * r1.v[2]);
+      m1.v[i] = ((A10.m[i][0] * r0.v[0] + A10.m[i][1] * r0.v[1]) + (A10.m[i][2] * r0.v[2] + A11.m[i][0] * r1.v[0])) +
+                (A11.m[i][1] * r1.v[1] + A11.m[i][2] * r1.v[2]);
+    }
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       M.m[i][0] = m0.v[i];
@@ -259,6 +271,7 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
     if (same1) break;                // fixed point: every later iterate equals it
     if (same2) { cyc2 = true; break; }  // 2-cycle: iterates alternate
   }
+  if (steps) *steps = k;
   // state after n_steps: (r0, r1) = iterate n_steps, (q0, q1) = iterate n_steps - 1
   if (k <= n_steps && cyc2 && ((n_steps - k) & 1)) {
     const V3 a0 = r0, a1 = r1;
@@ -296,8 +309,17 @@ __device__ __forceinline__ double polyval(const double* p, int degree, double x)
 }
 
 // solve_poly_approx for degree <= 4, unrolled over degrees 1..4 (no recursion)
+// The outer brackets [-1000, r_1] and [r_n, 1000] are shrunk to the Cauchy
+// bound 1 + max|p_i / p_deg| when it is smaller: no real root lies beyond it
+// (nor, by Gauss-Lucas, a derivative root), so the sign test and the bracketed
+// root are unchanged while the safeguarded Newton needs far fewer steps.
 __device__ int solve_poly_level(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
-  const double MAX_ROOT = 1000;
+  double MAX_ROOT = 1000;
+  if (p[degree] != 0) {
+    double cb = 0;
+    for (int i = 0; i < degree; i++) cb = fmax(cb, fabs(p[i] / p[degree]));
+    MAX_ROOT = fmin(MAX_ROOT, 1 + cb);
+  }
   double p_der[4];
   for (int i = 0; i < degree; i++) p_der[i] = (i + 1) * p[i + 1];
   int n = 0;
@@ -500,15 +522,20 @@ __device__ void estimate_tag_pose(const double H[9], const double corners[4][2],
     R1.m[1][c] = -R1.m[1][c];
     R1.m[2][c] = -R1.m[2][c];
   }
-  const double err1 = orthogonal_iteration(v, p, &t1, &R1, 50);
+  int k1 = 0, k2 = 0;
+  const double err1 = orthogonal_iteration(v, p, &t1, &R1, 50, &k1);
   if (stamps) stamps[2] = wall_clock64();
   M3 R2;
   V3 t2 = {{0, 0, 0}};
   double err2 = HUGE_VAL;
   const bool amb = fix_pose_ambiguities(v, p, t1, R1, &R2);
   if (stamps) stamps[3] = wall_clock64();
-  if (amb) err2 = orthogonal_iteration(v, p, &t2, &R2, 50);
-  if (stamps) stamps[4] = wall_clock64();
+  if (amb) err2 = orthogonal_iteration(v, p, &t2, &R2, 50, &k2);
+  if (stamps) {
+    stamps[4] = wall_clock64();
+    stamps[8] = k1;
+    stamps[9] = k2;
+  }
   const bool second = !(err1 <= err2);
   const M3& R = second ? R2 : R1;
   const V3& t = second ? t2 : t1;

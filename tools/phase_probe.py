@@ -20,6 +20,7 @@ det = rva.GpuDetector(W, H, max_batch=B)
 for rep in range(3):
     det.detect_device(d_frames.data_ptr(), frames[0].nbytes, B)
     p = det.copy_probe().astype(np.int64)
-    nz = [i for i in range(64) if p[i]]
+    nz = [i for i in range(64) if p[i] and i not in (24, 25)]
+    print("  oi steps", p[24], p[25])
     t0 = p[nz[0]]
     print("rep %d:" % rep, " ".join("%d:%.2fus" % (i, (p[i] - t0) / 100.0) for i in nz))
