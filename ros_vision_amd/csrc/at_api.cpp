@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "../../include/at_api.h"
@@ -59,6 +60,8 @@ struct at_detector {
   int last_nframes;
   int pending;
   hipEvent_t ev_done;
+  int use_graphs;                         // replay the launch sequence as a hipGraph (AT_NO_GRAPH=1 disables)
+  std::map<int, hipGraphExec_t> graphs;   // key: nframes * 4 + fmt
   int profiling;
   hipEvent_t ev_stage[kNumStages + 1];
   double stage_ms[kNumStages];
@@ -131,6 +134,8 @@ void at_destroy(at_detector* d) {
   if (!d) return;
   (void)hipSetDevice(d->device);
   if (d->st) (void)hipStreamSynchronize(d->st);
+  for (auto& kv : d->graphs) (void)hipGraphExecDestroy(kv.second);
+  d->graphs.clear();
   for (void* p : d->allocs) (void)hipFree(p);
   if (d->h_ftab) (void)hipHostFree(d->h_ftab);
   if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
@@ -179,6 +184,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
+  d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) return AT_E_INVALID;
   p.tag_size = cfg->tag_size;
 
@@ -359,14 +365,41 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
   return n;
 }
 
+// The per-batch sequence: frame table H2D, control block reset, the kernels,
+// control block + detections D2H (all to/from pinned buffers whose addresses
+// never change, so it can be captured once per (nframes, fmt) and replayed).
+static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev) {
+  hipError_t e;
+  if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
+  if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
+  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev))) return e;
+  if ((e = hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st))) return e;
+  return hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
+                        hipMemcpyDeviceToHost, st);
+}
+
 static int enqueue(at_detector* d, int nframes, int fmt) {
   hipStream_t st = d->st;
-  HIPCHK(hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st));
-  HIPCHK(launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, d->profiling ? d->ev_stage : nullptr));
-  HIPCHK(hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
-                        hipMemcpyDeviceToHost, st));
+  if (d->profiling || !d->use_graphs) {
+    HIPCHK(record_sequence(d, nframes, fmt, st, d->profiling ? d->ev_stage : nullptr));
+  } else {
+    const int key = nframes * 4 + fmt;
+    auto it = d->graphs.find(key);
+    if (it == d->graphs.end()) {
+      hipGraph_t graph = nullptr;
+      HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      const hipError_t rec = record_sequence(d, nframes, fmt, st, nullptr);
+      const hipError_t end = hipStreamEndCapture(st, &graph);
+      HIPCHK(rec);
+      HIPCHK(end);
+      hipGraphExec_t exec = nullptr;
+      const hipError_t inst = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      HIPCHK(inst);
+      it = d->graphs.emplace(key, exec).first;
+    }
+    HIPCHK(hipGraphLaunch(it->second, st));
+  }
   HIPCHK(hipEventRecord(d->ev_done, st));
   d->last_nframes = nframes;
   d->pending = 1;

@@ -551,3 +551,6 @@ __device__ void estimate_tag_pose(const double H[9], const double corners[4][2],
 
 }  // namespace pose
 }  // namespace at
+
+// back to the translation unit's -ffp-contract=off for everything after this header
+#pragma clang fp contract(off)

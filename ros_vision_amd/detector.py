@@ -279,6 +279,14 @@ class GpuDetector:
             _check(rc, "at_detect")
         return self._unpack(1)[0]
 
+    def detect_count(self, frame: np.ndarray, fmt: int = AT_FMT_YUYV):
+        """at_detect without building Python objects: returns the detection count
+        (the detections are in this detector's at_detection buffer)."""
+        rc = load_library().at_detect(self._h, frame.ctypes.data, fmt, self._out, self._cap, self._n)
+        if rc < 0 and rc != AT_E_CAPACITY:
+            _check(rc, "at_detect")
+        return self._n[0]
+
     def detect_batch(self, frames, fmt: int = AT_FMT_YUYV):
         frames = [np.ascontiguousarray(f, dtype=np.uint8) for f in frames]
         ptrs = (C.c_void_p * len(frames))(*[f.ctypes.data for f in frames])
@@ -288,13 +296,16 @@ class GpuDetector:
             _check(rc, "at_detect_batch")
         return self._unpack(len(frames))
 
-    def detect_device(self, dev_ptr: int, frame_stride: int, nframes: int, fmt: int = AT_FMT_YUYV):
+    def detect_device(self, dev_ptr: int, frame_stride: int, nframes: int, fmt: int = AT_FMT_YUYV,
+                      counts_only=False):
         """Frames already resident in device memory (e.g. a torch.cuda tensor's data_ptr())."""
         rc = load_library().at_detect_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt,
                                              self._out, self._cap, self._n)
         self._last_status = rc
         if rc < 0 and rc != AT_E_CAPACITY:
             _check(rc, "at_detect_device")
+        if counts_only:
+            return [self._n[f] for f in range(nframes)]
         return self._unpack(nframes)
 
     def enqueue_device(self, dev_ptr: int, frame_stride: int, nframes: int, fmt: int = AT_FMT_YUYV):
@@ -310,10 +321,15 @@ class GpuDetector:
         return [Pose(id=b.id, R=np.array(list(b.R)).reshape(3, 3), t=np.array(list(b.t)), err=b.err)
                 for b in buf[:min(n, self._cap)]]
 
-    def collect(self):
+    def collect(self, counts_only=False):
+        """at_collect: wait for the batch, run the host tail.  The detections land in
+        this detector's at_detection buffer; counts_only=True skips building Python
+        objects from it and returns the per-frame counts (what a C++ caller sees)."""
         rc = load_library().at_collect(self._h, self._out, self._cap, self._n)
         if rc < 0 and rc != AT_E_CAPACITY:
             _check(rc, "at_collect")
+        if counts_only:
+            return [self._n[f] for f in range(self._pending)]
         return self._unpack(self._pending)
 
     # ---- per-stage timing (the reference's CudaEvent stage timers,
