@@ -22,7 +22,7 @@
 namespace at {
 hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st, hipEvent_t* ev);
+                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join);
 
 struct CodeEntry {
   int id;
@@ -45,6 +45,8 @@ struct at_detector {
   int device;
   int nblobwg;
   hipStream_t st;
+  hipStream_t st2;          // fork/join branch for the small-blob kernel
+  hipEvent_t ev_fork, ev_join;
   DevBufs d;
   std::vector<void*> allocs;
   uint8_t* d_in;            // staging for host frames [B][max frame bytes]
@@ -134,6 +136,7 @@ void at_destroy(at_detector* d) {
   if (!d) return;
   (void)hipSetDevice(d->device);
   if (d->st) (void)hipStreamSynchronize(d->st);
+  if (d->st2) (void)hipStreamSynchronize(d->st2);
   for (auto& kv : d->graphs) (void)hipGraphExecDestroy(kv.second);
   d->graphs.clear();
   for (void* p : d->allocs) (void)hipFree(p);
@@ -143,6 +146,9 @@ void at_destroy(at_detector* d) {
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
   for (int i = 0; i <= kNumStages; i++)
     if (d->ev_stage[i]) (void)hipEventDestroy(d->ev_stage[i]);
+  if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+  if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+  if (d->st2) (void)hipStreamDestroy(d->st2);
   if (d->st) (void)hipStreamDestroy(d->st);
   delete d;
 }
@@ -195,6 +201,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipSetDevice(d->device) != hipSuccess) return fail(AT_E_HIP);
   if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
+  if (hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
+  if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
+  if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
   d->nblobwg = std::max(64, ncu * 2);
@@ -256,11 +265,15 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.workhead_small = d->d_ctrl + 6 * B + 5;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
-  // blob scratch: large teams (nblobwg x kSortCap) and small teams (8 x nblobwg x kSmallBlob) share it
-  const size_t nw = std::max((size_t)d->nblobwg * kSortCap, (size_t)d->nblobwg * 8 * kSmallBlob);
-  b.s_i32 = (int32_t*)dalloc(nw * 3 * 4);
-  b.s_i64 = (int64_t*)dalloc(nw * 3 * 8);
-  b.s_f64 = (double*)dalloc(nw * 2 * 8);
+  // blob scratch: large teams (nblobwg x kSortCap) and small teams (8 x nblobwg x kSmallBlob),
+  // disjoint because the two kernels run concurrently
+  const size_t nl = (size_t)d->nblobwg * kSortCap, ns = (size_t)d->nblobwg * 8 * kSmallBlob;
+  b.s_i32 = (int32_t*)dalloc(nl * 3 * 4);
+  b.s_i64 = (int64_t*)dalloc(nl * 3 * 8);
+  b.s_f64 = (double*)dalloc(nl * 2 * 8);
+  b.ss_i32 = (int32_t*)dalloc(ns * 3 * 4);
+  b.ss_i64 = (int64_t*)dalloc(ns * 3 * 8);
+  b.ss_f64 = (double*)dalloc(ns * 2 * 8);
   if (oom) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
   d->poses.assign(B * kMaxDets, at_pose{});
@@ -372,7 +385,8 @@ static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStrea
   hipError_t e;
   if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
   if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
-  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev))) return e;
+  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join)))
+    return e;
   if ((e = hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st))) return e;
   return hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
                         hipMemcpyDeviceToHost, st);

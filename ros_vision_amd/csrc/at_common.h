@@ -17,6 +17,10 @@ constexpr int kMaxDets = 128;          // candidate detections per frame
 constexpr int kMaxQuads = 2048;        // fitted-quad debug records per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
+// Blobs of more than kSmallBlob points: one workgroup each, 1024 threads for
+// small batches (latency: the biggest blob is the critical path), 256 for
+// large batches (throughput: more blobs in flight per CU).
+constexpr int kWideBlobMaxBatch = 8;
 constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wave-per-blob
 constexpr int kNMaxima = 10;
 
@@ -128,9 +132,12 @@ struct DevBufs {
   QuadCand* qcand;    // [qcand_cap]
   uint32_t qcand_cap;
   // per-workgroup scratch of the blob kernel
-  int32_t* s_i32;     // [nblobwg][3][kSortCap]  prefix Mx, My, W
+  int32_t* s_i32;     // [nblobwg][3][kSortCap]  prefix Mx, My, W        (large-blob teams)
   int64_t* s_i64;     // [nblobwg][3][kSortCap]  prefix Mxx, Myy, Mxy
   double* s_f64;      // [nblobwg][2][kSortCap]  errs, filtered errs
+  int32_t* ss_i32;    // [8*nblobwg][3][kSmallBlob] the same for the small-blob teams, which
+  int64_t* ss_i64;    // run concurrently with the large ones (separate regions)
+  double* ss_f64;
 };
 
 }  // namespace at

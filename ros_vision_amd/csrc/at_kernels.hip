@@ -909,21 +909,21 @@ struct MaxOp { template <typename T> __device__ T operator()(T a, T c) const { r
 struct AddOp { template <typename T> __device__ T operator()(T a, T c) const { return a + c; } };
 
 template <typename T, typename Op>
-__device__ T block_reduce(T v, Op op, T* s_tmp /* >= 4 */) {
+__device__ T block_reduce(T v, Op op, T* s_tmp /* >= NW */, int NW) {
   v = wave_reduce(v, op);
   const int w = threadIdx.x >> 6;
   __syncthreads();
   if (lane_id() == 0) s_tmp[w] = v;
   __syncthreads();
   T r = s_tmp[0];
-  for (int i = 1; i < kBlobThreads / 64; i++) r = op(r, s_tmp[i]);
+  for (int i = 1; i < NW; i++) r = op(r, s_tmp[i]);
   return r;
 }
 
-// inclusive block scan of one value per thread (256 threads); returns the
+// inclusive block scan of one value per thread (NW waves); returns the
 // inclusive prefix, *total = block sum
 template <typename T>
-__device__ T block_incl_scan(T v, T* s_tmp, T* total) {
+__device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -934,9 +934,12 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total) {
   __syncthreads();
   if (lane == 63) s_tmp[w] = v;
   __syncthreads();
-  T base = 0;
-  for (int i = 0; i < w; i++) base = base + s_tmp[i];
-  *total = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+  T base = 0, tot = 0;
+  for (int i = 0; i < NW; i++) {
+    if (i < w) base = base + s_tmp[i];
+    tot = tot + s_tmp[i];
+  }
+  *total = tot;
   return base + v;
 }
 
@@ -964,7 +967,7 @@ __device__ T team_reduce(T v, Op op, T* s_tmp) {
   if constexpr (NT == 64) {
     return wave_reduce(v, op);
   } else {
-    return block_reduce(v, op, s_tmp);
+    return block_reduce(v, op, s_tmp, NT / 64);
   }
 }
 
@@ -980,7 +983,7 @@ __device__ T team_incl_scan(T v, T* s_tmp, T* total) {
     *total = __shfl(v, 63);
     return v;
   } else {
-    return block_incl_scan(v, s_tmp, total);
+    return block_incl_scan(v, s_tmp, total, NT / 64);
   }
 }
 
@@ -1139,11 +1142,11 @@ __device__ __forceinline__ LineFitOut fit_line_v(const Moments& m) {
 template <int CAP>
 struct BlobShared {
   uint64_t keys[CAP];  // point sort keys, later peak keys
-  double red_f64[4];
-  int64_t red_i64[4];
-  uint32_t red_u32[4];
-  int32_t red_i32[4];
-  uint32_t red_idx[4];
+  double red_f64[16];
+  int64_t red_i64[16];
+  uint32_t red_u32[16];
+  int32_t red_i32[16];
+  uint32_t red_idx[16];
   uint32_t item, nwork, npeaks;
   int32_t pi[16];
   double e01[7][7];
@@ -1474,25 +1477,27 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   team_sync<NT>();
 }
 
-__device__ __forceinline__ BlobScratch blob_scratch(const DevBufs& b, size_t team, int cap) {
+__device__ __forceinline__ BlobScratch blob_scratch(int32_t* s_i32, int64_t* s_i64, double* s_f64, size_t team,
+                                                    int cap) {
   BlobScratch P;
-  P.Mx = b.s_i32 + (team * 3 + 0) * cap;
-  P.My = b.s_i32 + (team * 3 + 1) * cap;
-  P.W = b.s_i32 + (team * 3 + 2) * cap;
-  P.Mxx = b.s_i64 + (team * 3 + 0) * cap;
-  P.Myy = b.s_i64 + (team * 3 + 1) * cap;
-  P.Mxy = b.s_i64 + (team * 3 + 2) * cap;
-  P.err = b.s_f64 + (team * 2 + 0) * cap;
-  P.filt = b.s_f64 + (team * 2 + 1) * cap;
+  P.Mx = s_i32 + (team * 3 + 0) * cap;
+  P.My = s_i32 + (team * 3 + 1) * cap;
+  P.W = s_i32 + (team * 3 + 2) * cap;
+  P.Mxx = s_i64 + (team * 3 + 0) * cap;
+  P.Myy = s_i64 + (team * 3 + 1) * cap;
+  P.Mxy = s_i64 + (team * 3 + 2) * cap;
+  P.err = s_f64 + (team * 2 + 0) * cap;
+  P.filt = s_f64 + (team * 2 + 1) * cap;
   return P;
 }
 
 // K9a (large blobs, > kSmallBlob points): one blob per 256-thread workgroup
 // iteration, persistent over the large work list.
-__global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params prm) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<kSortCap> S;
   const int tid = threadIdx.x;
-  const BlobScratch P = blob_scratch(b, blockIdx.x, kSortCap);
+  const BlobScratch P = blob_scratch(b.s_i32, b.s_i64, b.s_f64, blockIdx.x, kSortCap);
   if (tid == 0) S.nwork = *b.nwork;
   __syncthreads();
   const uint32_t nwork = S.nwork;
@@ -1502,7 +1507,7 @@ __global__ __launch_bounds__(kBlobThreads) void k_blob(DevBufs b, Geom g, Params
     const uint32_t item = S.item;
     __syncthreads();
     if (item >= nwork) break;
-    blob_item<kBlobThreads, kSortCap>(b, g, prm, S, P, b.work[item]);
+    blob_item<NT, kSortCap>(b, g, prm, S, P, b.work[item]);
   }
 }
 
@@ -1513,7 +1518,7 @@ __global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params pr
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   BlobShared<kSmallBlob>& S = Ss[wave];
-  const BlobScratch P = blob_scratch(b, (size_t)blockIdx.x * 4 + wave, kSmallBlob);
+  const BlobScratch P = blob_scratch(b.ss_i32, b.ss_i64, b.ss_f64, (size_t)blockIdx.x * 4 + wave, kSmallBlob);
   const uint32_t nwork = *b.nwork_small;
   while (true) {
     uint32_t item = 0;
@@ -1852,8 +1857,11 @@ __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
                           (prm.probe && f == 0 && i == 0) ? b.probe + 16 : nullptr);
 }
 
+// st2/fork/join: a second stream on which the small-blob kernel runs beside
+// the large-blob one (both read k_group's output, neither reads the other's);
+// with stage profiling (ev != nullptr) everything stays on st, in order.
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st, hipEvent_t* ev) {
+                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join) {
   int e = 0;
   auto mark = [&]() {
     if (ev) (void)hipEventRecord(ev[e++], st);
@@ -1887,10 +1895,22 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   mark();
   hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
   mark();
-  hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st, b, g, prm);
-  mark();
-  hipLaunchKernelGGL(k_blob, dim3(nblobwg), dim3(kBlobThreads), 0, st, b, g, prm);
-  mark();
+  if (ev || !st2) {
+    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st, b, g, prm);
+    mark();
+    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, st, b, g, prm);
+    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, st, b, g, prm);
+    mark();
+  } else {
+    hipError_t e;
+    if ((e = hipEventRecord(fork, st))) return e;
+    if ((e = hipStreamWaitEvent(st2, fork, 0))) return e;
+    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st2, b, g, prm);
+    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, st, b, g, prm);
+    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, st, b, g, prm);
+    if ((e = hipEventRecord(join, st2))) return e;
+    if ((e = hipStreamWaitEvent(st, join, 0))) return e;
+  }
   hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm);
   mark();
   if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
