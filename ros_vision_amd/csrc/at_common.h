@@ -22,6 +22,7 @@ constexpr int kBlobThreads = 256;
 // large batches (throughput: more blobs in flight per CU).
 constexpr int kWideBlobMaxBatch = 8;
 constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wave-per-blob
+constexpr int kLdsBlob = 256;          // ... and keep their prefix moments / errors in LDS up to this many
 constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------

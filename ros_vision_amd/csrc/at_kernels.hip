@@ -26,6 +26,10 @@
 #include "at_common.h"
 #include "at_pose.h"
 
+#ifndef AT_LDS_BLOB
+#define AT_LDS_BLOB 0  // small-blob prefix moments in LDS (trades occupancy for latency)
+#endif
+
 namespace at {
 
 // ---------------------------------------------------------------------------
@@ -700,7 +704,24 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
   __syncthreads();
   stamp(2);
-  block_bitonic_sort<uint64_t, 1024>(s_list, np2);
+  if (n <= 1024) {
+    // rank sort (keys are unique: the slot rides in the low bits); t_key is free
+    // once the lookup table has been written out above
+    const uint64_t key = tid < (int)n ? s_list[tid] : 0;
+    uint32_t r = 0;
+    if (tid < (int)n) {
+      int j = 0;
+      for (; j + 4 <= (int)n; j += 4)
+        r += (s_list[j] < key) + (s_list[j + 1] < key) + (s_list[j + 2] < key) + (s_list[j + 3] < key);
+      for (; j < (int)n; j++) r += s_list[j] < key;
+      t_key[r] = key;
+    }
+    __syncthreads();
+    if (tid < (int)n) s_list[tid] = t_key[tid];
+    __syncthreads();
+  } else {
+    block_bitonic_sort<uint64_t, 1024>(s_list, np2);
+  }
   stamp(3);
   // counts in rank order, exclusive scan -> offsets
   for (int i = tid; i < kMaxPairs; i += 1024) s_cnt[i] = i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u;
@@ -1123,8 +1144,6 @@ __device__ __forceinline__ uint64_t rotate90_36(uint64_t w) {
 
 // lexicographic 4-combinations of 10 maxima == Unrank (line_fit_filter.cu:709-728)
 __constant__ uint8_t c_combo[210][4] = {{0,1,2,3},{0,1,2,4},{0,1,2,5},{0,1,2,6},{0,1,2,7},{0,1,2,8},{0,1,2,9},{0,1,3,4},{0,1,3,5},{0,1,3,6},{0,1,3,7},{0,1,3,8},{0,1,3,9},{0,1,4,5},{0,1,4,6},{0,1,4,7},{0,1,4,8},{0,1,4,9},{0,1,5,6},{0,1,5,7},{0,1,5,8},{0,1,5,9},{0,1,6,7},{0,1,6,8},{0,1,6,9},{0,1,7,8},{0,1,7,9},{0,1,8,9},{0,2,3,4},{0,2,3,5},{0,2,3,6},{0,2,3,7},{0,2,3,8},{0,2,3,9},{0,2,4,5},{0,2,4,6},{0,2,4,7},{0,2,4,8},{0,2,4,9},{0,2,5,6},{0,2,5,7},{0,2,5,8},{0,2,5,9},{0,2,6,7},{0,2,6,8},{0,2,6,9},{0,2,7,8},{0,2,7,9},{0,2,8,9},{0,3,4,5},{0,3,4,6},{0,3,4,7},{0,3,4,8},{0,3,4,9},{0,3,5,6},{0,3,5,7},{0,3,5,8},{0,3,5,9},{0,3,6,7},{0,3,6,8},{0,3,6,9},{0,3,7,8},{0,3,7,9},{0,3,8,9},{0,4,5,6},{0,4,5,7},{0,4,5,8},{0,4,5,9},{0,4,6,7},{0,4,6,8},{0,4,6,9},{0,4,7,8},{0,4,7,9},{0,4,8,9},{0,5,6,7},{0,5,6,8},{0,5,6,9},{0,5,7,8},{0,5,7,9},{0,5,8,9},{0,6,7,8},{0,6,7,9},{0,6,8,9},{0,7,8,9},{1,2,3,4},{1,2,3,5},{1,2,3,6},{1,2,3,7},{1,2,3,8},{1,2,3,9},{1,2,4,5},{1,2,4,6},{1,2,4,7},{1,2,4,8},{1,2,4,9},{1,2,5,6},{1,2,5,7},{1,2,5,8},{1,2,5,9},{1,2,6,7},{1,2,6,8},{1,2,6,9},{1,2,7,8},{1,2,7,9},{1,2,8,9},{1,3,4,5},{1,3,4,6},{1,3,4,7},{1,3,4,8},{1,3,4,9},{1,3,5,6},{1,3,5,7},{1,3,5,8},{1,3,5,9},{1,3,6,7},{1,3,6,8},{1,3,6,9},{1,3,7,8},{1,3,7,9},{1,3,8,9},{1,4,5,6},{1,4,5,7},{1,4,5,8},{1,4,5,9},{1,4,6,7},{1,4,6,8},{1,4,6,9},{1,4,7,8},{1,4,7,9},{1,4,8,9},{1,5,6,7},{1,5,6,8},{1,5,6,9},{1,5,7,8},{1,5,7,9},{1,5,8,9},{1,6,7,8},{1,6,7,9},{1,6,8,9},{1,7,8,9},{2,3,4,5},{2,3,4,6},{2,3,4,7},{2,3,4,8},{2,3,4,9},{2,3,5,6},{2,3,5,7},{2,3,5,8},{2,3,5,9},{2,3,6,7},{2,3,6,8},{2,3,6,9},{2,3,7,8},{2,3,7,9},{2,3,8,9},{2,4,5,6},{2,4,5,7},{2,4,5,8},{2,4,5,9},{2,4,6,7},{2,4,6,8},{2,4,6,9},{2,4,7,8},{2,4,7,9},{2,4,8,9},{2,5,6,7},{2,5,6,8},{2,5,6,9},{2,5,7,8},{2,5,7,9},{2,5,8,9},{2,6,7,8},{2,6,7,9},{2,6,8,9},{2,7,8,9},{3,4,5,6},{3,4,5,7},{3,4,5,8},{3,4,5,9},{3,4,6,7},{3,4,6,8},{3,4,6,9},{3,4,7,8},{3,4,7,9},{3,4,8,9},{3,5,6,7},{3,5,6,8},{3,5,6,9},{3,5,7,8},{3,5,7,9},{3,5,8,9},{3,6,7,8},{3,6,7,9},{3,6,8,9},{3,7,8,9},{4,5,6,7},{4,5,6,8},{4,5,6,9},{4,5,7,8},{4,5,7,9},{4,5,8,9},{4,6,7,8},{4,6,7,9},{4,6,8,9},{4,7,8,9},{5,6,7,8},{5,6,7,9},{5,6,8,9},{5,7,8,9},{6,7,8,9}};
-// (m0, m1) pairs of Compute{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7}Fit / Get{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7} (line_fit_filter.cu:731-743, 936-972)
-__constant__ uint8_t c_m0m1[28][2] = {{0,1},{0,2},{0,3},{0,4},{0,5},{0,6},{0,7},{1,2},{1,3},{1,4},{1,5},{1,6},{1,7},{2,3},{2,4},{2,5},{2,6},{2,7},{3,4},{3,5},{3,6},{3,7},{4,5},{4,6},{4,7},{5,6},{5,7},{6,7}};
 
 struct LineFitOut {
   double err, mse;
@@ -1149,30 +1168,35 @@ struct BlobShared {
   uint32_t red_idx[16];
   uint32_t item, nwork, npeaks;
   int32_t pi[16];
-  double e01[7][7];
-  double lp01[7][7][2];
+  // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
+  // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0)
+  double seg_err[kNMaxima][kNMaxima];
+  double seg_mse[kNMaxima][kNMaxima];
+  double seg_p[kNMaxima][kNMaxima][2];
   double lines[4][4];
 };
 
 // Processes one work item (frame, pair rank) with a team of NT threads.
 template <int NT, int CAP>
 __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<CAP>& S,
-                          const BlobScratch& P, uint32_t w) {
+                          const BlobScratch& Pg, const BlobScratch* Pl, uint32_t lcap, uint32_t w, uint32_t* pacc) {
   const int tid = team_rank<NT>();
   const uint32_t lane = lane_id();
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k])
   uint64_t t_last = prm.probe ? wall_clock64() : 0;
-  auto phase = [&](int k) {
+  auto phase = [&](int k) {  // accumulated per team in registers, flushed once per kernel
     if (prm.probe && tid == 0) {
       const uint64_t now = wall_clock64();
-      atomicAdd((unsigned long long*)&b.probe[64 + (NT > 64 ? 16 : 0) + k], (unsigned long long)(now - t_last));
-      atomicAdd((unsigned long long*)&b.probe[96 + (NT > 64 ? 16 : 0) + k], 1ull);
+      pacc[k] += (uint32_t)(now - t_last);
+      pacc[10 + k] += 1;
       t_last = now;
     }
   };
     const int f = (int)(w >> 16);
     const uint32_t rank = w & 0xffff;
     const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+    // prefix moments / errors in LDS when they fit the team's LDS scratch
+    const BlobScratch& P = (Pl && n <= lcap) ? *Pl : Pg;
     const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
     uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
     const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
@@ -1342,15 +1366,16 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       S.pi[r] = v;
     }
     team_sync<NT>();
-    for (int c = tid; cnt >= 4 && c < 28; c += NT) {
-      const int m0 = c_m0m1[c][0], m1 = c_m0m1[c][1];
-      if (m1 < kNMaxima && m1 < cnt) {
-        const LineFitOut o = fit_line_v<false, true>(read_moments(P, n, S.pi[m0], S.pi[m1]));
-        S.e01[m0][m1 - 1] = o.mse > (double)prm.max_line_fit_mse ? DBL_MAX : o.err;
-        S.lp01[m0][m1 - 1][0] = o.p23[0];
-        S.lp01[m0][m1 - 1][1] = o.p23[1];
-      } else {
-        S.e01[m0][m1 - 1] = DBL_MAX;
+    // every segment a combination can use, fitted once (FitLine on the same
+    // moments as QuadFitCalculator's per-combination fits: identical results)
+    for (int c = tid; cnt >= 4 && c < kNMaxima * kNMaxima; c += NT) {
+      const int a = c / kNMaxima, bb = c % kNMaxima;
+      if (a != bb && a < cnt && bb < cnt) {
+        const LineFitOut o = fit_line_v<false, true>(read_moments(P, n, S.pi[a], S.pi[bb]));
+        S.seg_err[a][bb] = o.err;
+        S.seg_mse[a][bb] = o.mse;
+        S.seg_p[a][bb][0] = o.p23[0];
+        S.seg_p[a][bb][1] = o.p23[1];
       }
     }
     team_sync<NT>();
@@ -1359,21 +1384,17 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     // 210 lexicographic combinations; each lane keeps its first minimum
     double err = DBL_MAX;
     uint32_t bt = 0xffffffffu;
+    const double mse_max = (double)prm.max_line_fit_mse;
     for (int c = tid; c < 210; c += NT) {
       double e4 = DBL_MAX;
       if (cnt >= 4) {
         const int m0 = c_combo[c][0], m1 = c_combo[c][1], m2 = c_combo[c][2], m3 = c_combo[c][3];
-        const double e01 = S.e01[m0][m1 - 1];
-        if (m3 < cnt && e01 != DBL_MAX) {
-          const LineFitOut o12 = fit_line_v<false, true>(read_moments(P, n, S.pi[m1], S.pi[m2]));
-          if (!(o12.mse > (double)prm.max_line_fit_mse)) {
-            const double dot = S.lp01[m0][m1 - 1][0] * o12.p23[0] + S.lp01[m0][m1 - 1][1] * o12.p23[1];
+        if (m3 < cnt && !(S.seg_mse[m0][m1] > mse_max)) {
+          if (!(S.seg_mse[m1][m2] > mse_max)) {
+            const double dot = S.seg_p[m0][m1][0] * S.seg_p[m1][m2][0] + S.seg_p[m0][m1][1] * S.seg_p[m1][m2][1];
             if (!(fabs(dot) > prm.cos_critical_rad)) {
-              const LineFitOut o23 = fit_line_v<false, false>(read_moments(P, n, S.pi[m2], S.pi[m3]));
-              if (!(o23.mse > (double)prm.max_line_fit_mse)) {
-                const LineFitOut o30 = fit_line_v<false, false>(read_moments(P, n, S.pi[m3], S.pi[m0]));
-                if (!(o30.mse > (double)prm.max_line_fit_mse)) e4 = e01 + o12.err + o23.err + o30.err;
-              }
+              if (!(S.seg_mse[m2][m3] > mse_max) && !(S.seg_mse[m3][m0] > mse_max))
+                e4 = S.seg_err[m0][m1] + S.seg_err[m1][m2] + S.seg_err[m2][m3] + S.seg_err[m3][m0];
             }
           }
         }
@@ -1493,8 +1514,18 @@ __device__ __forceinline__ BlobScratch blob_scratch(int32_t* s_i32, int64_t* s_i
 
 // K9a (large blobs, > kSmallBlob points): one blob per 256-thread workgroup
 // iteration, persistent over the large work list.
+__device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm, const uint32_t* pacc, int base,
+                                            bool leader) {
+  if (!prm.probe || !leader) return;
+  for (int k = 0; k < 10; k++) {
+    if (pacc[k]) atomicAdd((unsigned long long*)&b.probe[base + k], (unsigned long long)pacc[k]);
+    if (pacc[10 + k]) atomicAdd((unsigned long long*)&b.probe[base + 32 + k], (unsigned long long)pacc[10 + k]);
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
+  uint32_t pacc[20] = {0};
   __shared__ BlobShared<kSortCap> S;
   const int tid = threadIdx.x;
   const BlobScratch P = blob_scratch(b.s_i32, b.s_i64, b.s_f64, blockIdx.x, kSortCap);
@@ -1507,26 +1538,41 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
     const uint32_t item = S.item;
     __syncthreads();
     if (item >= nwork) break;
-    blob_item<NT, kSortCap>(b, g, prm, S, P, b.work[item]);
+    blob_item<NT, kSortCap>(b, g, prm, S, P, nullptr, 0, b.work[item], pacc);
   }
+  probe_flush(b, prm, pacc, 80, tid == 0);
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
 // waves per workgroup, persistent over the small work list.
 __global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params prm) {
+  uint32_t pacc[20] = {0};
   __shared__ BlobShared<kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   BlobShared<kSmallBlob>& S = Ss[wave];
   const BlobScratch P = blob_scratch(b.ss_i32, b.ss_i64, b.ss_f64, (size_t)blockIdx.x * 4 + wave, kSmallBlob);
+#if AT_LDS_BLOB
+  __shared__ int32_t l_i32[4][3][kLdsBlob];
+  __shared__ int64_t l_i64[4][3][kLdsBlob];
+  __shared__ double l_f64[4][2][kLdsBlob];
+  BlobScratch L;
+  L.Mx = l_i32[wave][0]; L.My = l_i32[wave][1]; L.W = l_i32[wave][2];
+  L.Mxx = l_i64[wave][0]; L.Myy = l_i64[wave][1]; L.Mxy = l_i64[wave][2];
+  L.err = l_f64[wave][0]; L.filt = l_f64[wave][1];
+  const BlobScratch* PL = &L;
+#else
+  const BlobScratch* PL = nullptr;
+#endif
   const uint32_t nwork = *b.nwork_small;
   while (true) {
     uint32_t item = 0;
     if (lane == 0) item = atomicAdd(b.workhead_small, 1u);
     item = __shfl(item, 0);
     if (item >= nwork) break;
-    blob_item<64, kSmallBlob>(b, g, prm, S, P, b.work_small[item]);
+    blob_item<64, kSmallBlob>(b, g, prm, S, P, PL, kLdsBlob, b.work_small[item], pacc);
   }
+  probe_flush(b, prm, pacc, 64, lane == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1893,7 +1939,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   }
   hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
   mark();
-  hipLaunchKernelGGL(k_group, dim3(32, B), dim3(256), 0, st, b, g);
+  hipLaunchKernelGGL(k_group, dim3(std::max(32, std::min(512, 1024 / B)), B), dim3(256), 0, st, b, g);
   mark();
   if (ev || !st2) {
     hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st, b, g, prm);
