@@ -1168,6 +1168,8 @@ struct BlobShared {
   uint32_t red_idx[16];
   uint32_t item, nwork, npeaks;
   int32_t pi[16];
+  uint32_t bcnt[CAP / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
+  uint32_t bmax;
   // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
   // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0)
   double seg_err[kNMaxima][kNMaxima];
@@ -1175,6 +1177,90 @@ struct BlobShared {
   double seg_p[kNMaxima][kNMaxima][2];
   double lines[4][4];
 };
+
+// Sort of a blob's (theta, plane, y, x) keys: theta is near-uniform around the
+// blob centre, so the keys are bucketed by theta (counting sort: LDS histogram,
+// scan, scatter into the upper half of S.keys) and each key's final slot is its
+// bucket start + its rank inside the (small) bucket.  Exactly the order of a
+// full sort.  Returns false -- caller falls back to the bitonic sort -- when
+// the keys do not fit twice in S.keys or a bucket holds more than 32 keys.
+constexpr uint64_t kThetaSpan = 50265600;  // > max theta = rint((2 pi) * 8e6)
+
+template <int NT, int CAP>
+__device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
+  if (n < 64 || 2 * n > CAP) return false;
+  const int tid = team_rank<NT>();
+  int nb = 32;
+  while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= CAP/2
+  auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> 23) * (uint64_t)nb) / kThetaSpan); };
+  for (int i = tid; i < nb / 2; i += NT) S.bcnt[i] = 0;
+  team_sync<NT>();
+  for (int t = tid; t < n; t += NT) {
+    const uint32_t bk = bucket(S.keys[t]);
+    atomicAdd(&S.bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+  }
+  team_sync<NT>();
+  // exclusive scan of the nb counts: each thread owns nb/NT (or 1) consecutive buckets
+  const int per = nb >= NT ? nb / NT : 1;
+  const int b0 = tid * per;
+  uint32_t loc = 0, mx = 0;
+  uint32_t cval[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    cval[j] = 0;
+    if (j < per && b0 + j < nb) {
+      const uint32_t bb = (uint32_t)(b0 + j);
+      cval[j] = (S.bcnt[bb >> 1] >> ((bb & 1) * 16)) & 0xffffu;
+      loc += cval[j];
+      mx = cval[j] > mx ? cval[j] : mx;
+    }
+  }
+  uint32_t tot;
+  const uint32_t incl = team_incl_scan<NT>(loc, S.red_u32, &tot);
+  mx = team_reduce<NT>(mx, MaxOp(), S.red_u32);
+  if (mx > 32) return false;  // uniform across the team
+  team_sync<NT>();
+  // starts, written back in place (u16, < n)
+  uint32_t run = incl - loc;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    if (j < per && b0 + j < nb && (j & 1) == 0) {
+      const uint32_t bb = (uint32_t)(b0 + j);  // even: owns the whole word when per >= 2
+      if (per >= 2) {
+        const uint32_t s0 = run, s1 = run + cval[j];
+        S.bcnt[bb >> 1] = s0 | (s1 << 16);
+      }
+    }
+    if (j < per && b0 + j < nb) run += cval[j];
+  }
+  if (per == 1 && b0 < nb) {
+    // one bucket per thread: neighbours share a word; even lane writes both halves
+    const uint32_t mine = incl - loc;
+    const uint32_t other = __shfl_down(mine, 1);
+    if ((b0 & 1) == 0) S.bcnt[b0 >> 1] = mine | (other << 16);
+  }
+  team_sync<NT>();
+  uint64_t* T = S.keys + CAP / 2;
+  for (int t = tid; t < n; t += NT) {
+    const uint64_t k = S.keys[t];
+    const uint32_t bk = bucket(k);
+    const uint32_t old = atomicAdd(&S.bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+    T[(old >> ((bk & 1) * 16)) & 0xffffu] = k;
+  }
+  team_sync<NT>();
+  for (int s = tid; s < n; s += NT) {
+    const uint64_t k = T[s];
+    const uint32_t bk = bucket(k);
+    int lo = s, hi = s + 1;
+    while (lo > 0 && bucket(T[lo - 1]) == bk) lo--;
+    while (hi < n && bucket(T[hi]) == bk) hi++;
+    int r = lo;
+    for (int j = lo; j < hi; j++) r += T[j] < k;
+    S.keys[r] = k;
+  }
+  team_sync<NT>();
+  return true;
+}
 
 // Processes one work item (frame, pair rank) with a team of NT threads.
 template <int NT, int CAP>
@@ -1252,11 +1338,14 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       S.keys[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
                   ((uint64_t)bx << 1) | ((k >> 3) & 1);
     }
-    int np2 = 64;
-    while (np2 < (int)n) np2 <<= 1;
-    for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
     team_sync<NT>();
-    team_bitonic_sort<uint64_t, NT>(S.keys, np2);
+    if (!team_bucket_sort<NT, CAP>(S, (int)n)) {
+      int np2 = 64;
+      while (np2 < (int)n) np2 <<= 1;
+      for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
+      team_sync<NT>();
+      team_bitonic_sort<uint64_t, NT>(S.keys, np2);
+    }
     phase(2);
     if (prm.diag_stop == 2) return;
 
