@@ -49,6 +49,35 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_algorithmic_bytes(kernel, stats, W, H):
+    """Algorithmic bytes one launch of `kernel` must move, from the
+    batch's work counts."""
+    nf = stats.get("frames", 0)
+    Wd, Hd = W // 2, H // 2
+    if kernel == "k_pre":
+        return nf * (2 * W * H + W * H + Wd * Hd)           # YUYV in, gray + decimated out
+    if kernel == "k_boundary":
+        return nf * 5 * Wd * Hd + 8 * stats.get("boundary_points", 0)  # thr + labels in, points out
+    if kernel == "k_blob":
+        return 12 * stats.get("large_blob_points", 0)      # 8-B point key + 4 gradient bytes per point
+    if kernel == "k_blob_small":
+        return 12 * stats.get("small_blob_points", 0)
+    if kernel in ("k_thr_ccl", "k_ccl_final"):
+        return nf * 9 * Wd * Hd                            # dec/thr in, labels/sizes out
+    return None
+
+
+def pmc_traffic(W, H):
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        tj = json.load(open(tpath))
+        if tj.get("width") == W and tj.get("height") == H:
+            return tj
+    except Exception:
+        pass
+    return None
+
+
 def render_pool(args, rank):
     from ros_vision_amd import synth
     codes = dict(__import__("ros_vision_amd").family_entries())
@@ -127,6 +156,26 @@ def main():
         return ndet
 
     run(max(1, args.warmup))
+
+    # per-stage GPU time (HIP events between the kernels, serialized launch
+    # sequence) -- identifies the dominant kernel before the timed region
+    stages, stage_batches = {}, 0
+    if not args.no_stage_profile:
+        prof = dets[0]
+        prof.set_profiling(True)
+        for s in range(10):
+            prof.enqueue_device(batch_ptr(s), stride, B)
+            prof.collect()
+        stages, stage_batches = prof.stage_times()
+        prof.set_profiling(False)
+    dominant = max(stages, key=stages.get) if stages else "k_blob"
+    # live per-launch time of the dominant kernel inside the timed region
+    for d in dets:
+        d.set_kernel_timer(dominant)
+    run(1)
+    for d in dets:
+        d.set_kernel_timer(dominant)  # reset the accumulators
+
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -138,6 +187,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    kt = [d.kernel_time() for d in dets]
+    k_launches = sum(n for _, n in kt)
+    k_ms = sum(ms * n for ms, n in kt) / max(1, k_launches)
+    stats = dets[0].batch_stats()
+    for d in dets:
+        d.set_kernel_timer(None)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -168,37 +223,23 @@ def main():
     lat_h = np.array(lat_h or [0.0]) * 1e3
     lat_d = np.array(lat_d or [0.0]) * 1e3
 
-    # per-stage GPU time (HIP events on the detector's stream), separate pass
-    stages, stage_batches = {}, 0
-    if not args.no_stage_profile:
-        prof = dets[0]
-        prof.set_profiling(True)
-        for s in range(10):
-            prof.enqueue_device(batch_ptr(s), stride, B)
-            prof.collect()
-        stages, stage_batches = prof.stage_times()
-        prof.set_profiling(False)
-
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
 
-    algo_bytes_per_frame = 3 * W * H  # read YUYV 2WH + write gray WH
     per_gpu_fps = fps / world
-    achieved = per_gpu_fps * algo_bytes_per_frame / 1e9
     pipe_ms = sum(stages.values()) if stages else None
-    dominant = max(stages, key=stages.get) if stages else None
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            if tj.get("width") == W and tj.get("height") == H:
-                traffic = tj.get("hbm_bytes_per_frame")
-        except Exception:
-            traffic = None
+    kbytes = kernel_algorithmic_bytes(dominant, stats, W, H)
+    pmc = pmc_traffic(W, H)
+    k_traffic = None
+    if pmc and dominant:
+        kk = [v for k, v in pmc.get("kernels", {}).items() if k.split("<")[0] == dominant]
+        if kk:  # FETCH x2 (gfx950 correction) + WRITE, per frame -> per launch
+            k_traffic = round(B * sum(2 * v["fetch_bytes_per_frame"] + v["write_bytes_per_frame"] for v in kk))
+    k_achieved = kbytes / (k_ms * 1e-3) / 1e9 if (kbytes and k_ms > 0) else None
+    pipe_bytes = 3 * W * H  # read YUYV 2WH + write gray WH
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -222,10 +263,21 @@ def main():
         "p50_latency_hbm_ms": round(float(np.percentile(lat_d, 50)), 4),
         "p99_latency_hbm_ms": round(float(np.percentile(lat_d, 99)), 4),
         "detections_per_frame": round(ndet / total_frames, 3),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                     "bytes_per_frame": algo_bytes_per_frame,
-                     "note": "achieved = per-GPU frames/s x algorithmic bytes 3*W*H (BASELINE.md)"},
+        "roofline": {"bound": "hbm", "kernel": dominant,
+                     "achieved": round(k_achieved, 3) if k_achieved else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(k_achieved / HBM_PEAK_GBS, 6) if k_achieved else None,
+                     "traffic": k_traffic, "algorithmic_bytes_per_launch": kbytes,
+                     "avg_launch_ms": round(k_ms, 5), "launches_timed": k_launches,
+                     "note": "dominant kernel by stage time; HIP events around it on its stream in the timed "
+                             "region; algorithmic bytes per DESIGN.md section 4; traffic = PMC "
+                             "(2*FETCH_SIZE+WRITE_SIZE) per launch from profiles/pmc_traffic.json"},
+        "roofline_pipeline": {"bound": "hbm", "achieved": round(per_gpu_fps * pipe_bytes / 1e9, 3),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(per_gpu_fps * pipe_bytes / 1e9 / HBM_PEAK_GBS, 6),
+                              "traffic": pmc.get("hbm_bytes_per_frame") if pmc else None,
+                              "bytes_per_frame": pipe_bytes,
+                              "note": "SURVEY.md 8(d): per-GPU frames/s x 3*W*H; traffic = PMC bytes per frame"},
+        "batch_stats": stats,
         "stage_ms_per_batch": {k: round(v, 4) for k, v in stages.items()},
         "dominant_kernel": dominant,
         "pipeline_gpu_ms_per_batch": round(pipe_ms, 4) if pipe_ms else None,

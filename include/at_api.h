@@ -145,6 +145,20 @@ int at_set_profiling(at_detector *d, int enable);
 int at_stage_times(at_detector *d, double *ms, int cap);
 const char *at_stage_name(int stage);
 
+/* Live per-launch time of ONE kernel (stage index as at_stage_name) inside
+ * the normal launch sequence (concurrent streams; direct launches instead of
+ * the graph replay while a timer is set): HIP events bracket that kernel on
+ * its own stream.  stage -1 switches it off.
+ * at_kernel_time: mean ms per launch and number of launches since set. */
+int at_set_kernel_timer(at_detector *d, int stage);
+int at_kernel_time(at_detector *d, double *avg_ms, long long *launches);
+
+/* Work counts of the last collected batch: [0] frames, [1] boundary points,
+ * [2] blob pairs, [3] points processed by the small-blob kernel, [4] by the
+ * large-blob kernel, [5] fitted quads, [6] decoded candidates (pre-reconcile).
+ * Returns the number of entries written. */
+int at_batch_stats(at_detector *d, uint64_t *out, int cap);
+
 /* Tag pose of each detection of the last collected batch (row A23): the
  * reference node's estimate_tag_pose(&info_, &pose) per detection
  * (apriltags_cuda_detector.cu:425-436; AprilTag 3.x orthogonal iteration with

@@ -22,7 +22,8 @@
 namespace at {
 hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join);
+                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
+                           const KernelTimer* kt);
 
 struct CodeEntry {
   int id;
@@ -64,6 +65,9 @@ struct at_detector {
   hipEvent_t ev_done;
   int use_graphs;                         // replay the launch sequence as a hipGraph (AT_NO_GRAPH=1 disables)
   std::map<int, hipGraphExec_t> graphs;   // key: nframes * 4 + fmt
+  KernelTimer kt;                         // kt.stage < 0: off
+  double kt_ms;
+  long long kt_n;
   int profiling;
   hipEvent_t ev_stage[kNumStages + 1];
   double stage_ms[kNumStages];
@@ -146,6 +150,8 @@ void at_destroy(at_detector* d) {
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
   for (int i = 0; i <= kNumStages; i++)
     if (d->ev_stage[i]) (void)hipEventDestroy(d->ev_stage[i]);
+  if (d->kt.t0) (void)hipEventDestroy(d->kt.t0);
+  if (d->kt.t1) (void)hipEventDestroy(d->kt.t1);
   if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
   if (d->ev_join) (void)hipEventDestroy(d->ev_join);
   if (d->st2) (void)hipStreamDestroy(d->st2);
@@ -204,6 +210,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
+  d->kt.stage = -1;
+  if (hipEventCreate(&d->kt.t0) != hipSuccess || hipEventCreate(&d->kt.t1) != hipSuccess) return fail(AT_E_HIP);
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
   d->nblobwg = std::max(64, ncu * 2);
@@ -261,6 +269,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.nqcand = d->d_ctrl + 5 * B + 2;
   b.qhead = d->d_ctrl + 5 * B + 3;
   b.npent = d->d_ctrl + 5 * B + 4;
+  b.blob_pts = d->d_ctrl + 6 * B + 6;
   b.nwork_small = d->d_ctrl + 6 * B + 4;
   b.workhead_small = d->d_ctrl + 6 * B + 5;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
@@ -385,7 +394,8 @@ static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStrea
   hipError_t e;
   if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
   if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
-  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join)))
+  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
+                           d->kt.stage >= 0 ? &d->kt : nullptr)))
     return e;
   if ((e = hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st))) return e;
   return hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
@@ -394,7 +404,9 @@ static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStrea
 
 static int enqueue(at_detector* d, int nframes, int fmt) {
   hipStream_t st = d->st;
-  if (d->profiling || !d->use_graphs) {
+  // (HIP event-record nodes inside a captured graph do not carry timestamps, so
+  // a timed kernel is launched directly)
+  if (d->profiling || !d->use_graphs || d->kt.stage >= 0) {
     HIPCHK(record_sequence(d, nframes, fmt, st, d->profiling ? d->ev_stage : nullptr));
   } else {
     const int key = nframes * 4 + fmt;
@@ -431,6 +443,12 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
       d->stage_ms[i] += ms;
     }
     d->stage_batches++;
+  }
+  if (d->kt.stage >= 0) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, d->kt.t0, d->kt.t1));
+    d->kt_ms += ms;
+    d->kt_n++;
   }
   const int B = d->B;
   int rc = AT_OK;
@@ -524,6 +542,42 @@ int at_stage_times(at_detector* d, double* ms, int cap) {
 
 const char* at_stage_name(int stage) {
   return (stage >= 0 && stage < kNumStages) ? kStageNames[stage] : "";
+}
+
+int at_set_kernel_timer(at_detector* d, int stage) {
+  if (!d || stage < -1 || stage >= kNumStages) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));
+  d->kt.stage = stage;
+  d->kt_ms = 0;
+  d->kt_n = 0;
+  return AT_OK;
+}
+
+int at_kernel_time(at_detector* d, double* avg_ms, long long* launches) {
+  if (!d || !avg_ms) return AT_E_INVALID;
+  *avg_ms = d->kt_n ? d->kt_ms / (double)d->kt_n : 0.0;
+  if (launches) *launches = d->kt_n;
+  return AT_OK;
+}
+
+int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
+  if (!d || !out || cap < 1) return AT_E_INVALID;
+  if (d->pending) return AT_E_INVALID;
+  const int B = d->B;
+  uint64_t v[8] = {0};
+  v[0] = (uint64_t)d->last_nframes;
+  for (int f = 0; f < d->last_nframes; f++) {
+    v[1] += d->h_ctrl[f];
+    v[2] += d->h_ctrl[B + f];
+    v[5] += d->h_ctrl[3 * B + f];
+    v[6] += d->h_ctrl[2 * B + f];
+  }
+  v[3] = d->h_ctrl[6 * B + 6];
+  v[4] = d->h_ctrl[6 * B + 7];
+  const int n = std::min(cap, 7);
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return n;
 }
 
 int at_poses(at_detector* d, int frame, at_pose* out, int cap) {

@@ -1,6 +1,7 @@
 // at_common.h -- shared host/device definitions of the MI355X AprilTag stage.
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "at_detmath.h"
@@ -64,6 +65,12 @@ struct Params {
 };
 constexpr int kProbeWords = 256;
 
+// HIP events bracketing one kernel of the launch sequence (bench roofline).
+struct KernelTimer {
+  int stage;
+  hipEvent_t t0, t1;
+};
+
 // One detection candidate as produced on the device (before reconcile).
 struct DevDetection {
   int32_t id, hamming;
@@ -126,6 +133,7 @@ struct DevBufs {
   uint32_t* nwork;    // [1]
   uint32_t* workhead; // [1]
   uint64_t* probe;    // [kProbeWords] phase clock stamps (diagnostics)
+  uint32_t* blob_pts;       // [2] points processed by the small / large blob kernels (batch statistics)
   uint32_t* nwork_small;    // [1]
   uint32_t* workhead_small; // [1]
   uint32_t* nqcand;   // [1]

@@ -1281,6 +1281,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     const int f = (int)(w >> 16);
     const uint32_t rank = w & 0xffff;
     const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+    if (tid == 0) pacc[20] += n;  // points this team processed (batch statistics)
     // prefix moments / errors in LDS when they fit the team's LDS scratch
     const BlobScratch& P = (Pl && n <= lcap) ? *Pl : Pg;
     const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
@@ -1614,7 +1615,7 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
-  uint32_t pacc[20] = {0};
+  uint32_t pacc[21] = {0};
   __shared__ BlobShared<kSortCap> S;
   const int tid = threadIdx.x;
   const BlobScratch P = blob_scratch(b.s_i32, b.s_i64, b.s_f64, blockIdx.x, kSortCap);
@@ -1630,12 +1631,13 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
     blob_item<NT, kSortCap>(b, g, prm, S, P, nullptr, 0, b.work[item], pacc);
   }
   probe_flush(b, prm, pacc, 80, tid == 0);
+  if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
 // waves per workgroup, persistent over the small work list.
 __global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params prm) {
-  uint32_t pacc[20] = {0};
+  uint32_t pacc[21] = {0};
   __shared__ BlobShared<kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
@@ -1662,6 +1664,7 @@ __global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params pr
     blob_item<64, kSmallBlob>(b, g, prm, S, P, PL, kLdsBlob, b.work_small[item], pacc);
   }
   probe_flush(b, prm, pacc, 64, lane == 0);
+  if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1995,60 +1998,94 @@ __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
 // st2/fork/join: a second stream on which the small-blob kernel runs beside
 // the large-blob one (both read k_group's output, neither reads the other's);
 // with stage profiling (ev != nullptr) everything stays on st, in order.
+// kt (optional): HIP events bracketing one kernel (kt->stage, kStageNames
+// order) on the stream it runs on -- the live per-launch duration bench.py
+// reports for the roofline; recorded inside the captured graph as well.
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
-                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join) {
+                           hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
+                           const KernelTimer* kt) {
   int e = 0;
   auto mark = [&]() {
     if (ev) (void)hipEventRecord(ev[e++], st);
   };
+  auto tk = [&](int stage, hipStream_t s, int which) {
+    if (kt && kt->stage == stage) (void)hipEventRecord(which ? kt->t1 : kt->t0, s);
+  };
   mark();
   {
     dim3 blk(64, 4), grd((g.TW + 63) / 64, (g.TH + 3) / 4, B);
+    tk(0, st, 0);
     if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
     else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
     else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
+    tk(0, st, 1);
   }
   mark();
   {
     dim3 grd(g.CTX, g.CTY, B);
+    tk(1, st, 0);
     hipLaunchKernelGGL(k_thr_ccl, grd, dim3(256), 0, st, b, g, prm);
+    tk(1, st, 1);
     mark();
+    tk(2, st, 0);
     hipLaunchKernelGGL(k_ccl_border, grd, dim3(64), 0, st, b, g);
+    tk(2, st, 1);
     mark();
   }
   {
     dim3 blk(64, 4), grd((g.BW + 63) / 64, (g.BH + 3) / 4, B);
+    tk(3, st, 0);
     hipLaunchKernelGGL(k_ccl_final, grd, blk, 0, st, b, g);
+    tk(3, st, 1);
     mark();
   }
   {
     dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows), B);
+    tk(4, st, 0);
     hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
+    tk(4, st, 1);
     mark();
   }
+  tk(5, st, 0);
   hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
+  tk(5, st, 1);
   mark();
+  tk(6, st, 0);
   hipLaunchKernelGGL(k_group, dim3(std::max(32, std::min(512, 1024 / B)), B), dim3(256), 0, st, b, g);
+  tk(6, st, 1);
   mark();
+  auto blob_large = [&](hipStream_t s) {
+    tk(8, s, 0);
+    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, s, b, g, prm);
+    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, s, b, g, prm);
+    tk(8, s, 1);
+  };
+  auto blob_small = [&](hipStream_t s) {
+    tk(7, s, 0);
+    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    tk(7, s, 1);
+  };
   if (ev || !st2) {
-    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st, b, g, prm);
+    blob_small(st);
     mark();
-    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, st, b, g, prm);
-    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, st, b, g, prm);
+    blob_large(st);
     mark();
   } else {
     hipError_t e;
     if ((e = hipEventRecord(fork, st))) return e;
     if ((e = hipStreamWaitEvent(st2, fork, 0))) return e;
-    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, st2, b, g, prm);
-    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, st, b, g, prm);
-    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, st, b, g, prm);
+    blob_small(st2);
+    blob_large(st);
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }
+  tk(9, st, 0);
   hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm);
+  tk(9, st, 1);
   mark();
+  tk(10, st, 0);
   if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
+  tk(10, st, 1);
   mark();
   return hipGetLastError();
 }

@@ -30,6 +30,7 @@ EXPORTS = [
     "at_enqueue_device", "at_collect", "at_frame_status", "at_debug_copy", "at_destroy",
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
+    "at_set_kernel_timer", "at_kernel_time", "at_batch_stats",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -168,6 +169,9 @@ def load_library(path: str = LIB_PATH):
     L.at_stage_name.restype = C.c_char_p
     L.at_stage_name.argtypes = [C.c_int]
     L.at_poses.argtypes = [C.c_void_p, C.c_int, C.POINTER(AtPose), C.c_int]
+    L.at_set_kernel_timer.argtypes = [C.c_void_p, C.c_int]
+    L.at_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
+    L.at_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     L.at_tag_detections.argtypes = [C.POINTER(AtPose), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                     C.POINTER(AtTagDetection)]
     _LIB = L
@@ -344,6 +348,30 @@ class GpuDetector:
         n = _check(L.at_stage_times(self._h, buf, 32), "at_stage_times")
         batches = int(buf[n]) if n < 32 else 0
         return {L.at_stage_name(i).decode(): buf[i] for i in range(n)}, batches
+
+    def set_kernel_timer(self, stage_name=None):
+        """Time one kernel live inside the normal launch sequence (None: off)."""
+        L = load_library()
+        stage = -1
+        if stage_name is not None:
+            names = [L.at_stage_name(i).decode() for i in range(32)]
+            stage = names.index(stage_name)
+        _check(L.at_set_kernel_timer(self._h, stage), "at_set_kernel_timer")
+
+    def kernel_time(self):
+        """(mean ms per launch, launches) of the timed kernel."""
+        ms, n = C.c_double(), C.c_longlong()
+        _check(load_library().at_kernel_time(self._h, C.byref(ms), C.byref(n)), "at_kernel_time")
+        return ms.value, n.value
+
+    BATCH_STATS = ("frames", "boundary_points", "pairs", "small_blob_points", "large_blob_points",
+                   "quads", "candidates")
+
+    def batch_stats(self):
+        """Work counts of the last collected batch (see at_batch_stats)."""
+        buf = (C.c_uint64 * 8)()
+        n = _check(load_library().at_batch_stats(self._h, buf, 8), "at_batch_stats")
+        return dict(zip(self.BATCH_STATS, [int(x) for x in buf[:n]]))
 
     def detections(self, frame=0):
         """GpuDetector::Detections (apriltag_gpu.h:93), sorted by id."""
