@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec + p50 per-frame latency, 1280x720 AprilTag detect at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+C_SIZEOF_DET = 168     # sizeof(at_detection)
 
 
 def parse():
@@ -46,6 +47,10 @@ def parse():
     ap.add_argument("--latency-frames", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
+    ap.add_argument("--ingest", choices=["local", "scatter"], default="local",
+                    help="local: every rank renders its own frames into its HBM (weak scaling, no data-path "
+                         "collective); scatter: frames live on rank 0 and are scattered each step over RCCL "
+                         "(north-star topology), detection records gathered back to rank 0")
     return ap.parse_args()
 
 
@@ -115,25 +120,61 @@ def cpu_baseline(frames, width, height):
 
 def main():
     args = parse()
+    # stdout carries exactly one JSON line: libraries that print banners to fd 1
+    # (RCCL prints its version block at communicator init) are sent to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch  # device memory + torch.distributed; loads the HIP runtime first
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    if world > 1 or args.ingest == "scatter":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
 
     import ros_vision_amd as rva
+    from ros_vision_amd import multigpu
     W, H, B = args.width, args.height, args.batch
     assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
+    scatter = args.ingest == "scatter"
     frames = render_pool(args, rank)
     d_frames = torch.from_numpy(frames).to("cuda")
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
     npool = args.pool
     dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank) for _ in range(2)]
+    ingest = None
+    if scatter:
+        # rank 0 holds every rank's frame pool in its HBM; each step scatters B frames per rank
+        root_pool = None
+        if rank == 0:
+            root_pool = torch.empty((world, npool) + frames.shape[1:], dtype=torch.uint8, device="cuda")
+            for r in range(world):
+                root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames)
+        ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda")
+        rec_cap = 32  # detection records per frame gathered to rank 0 (fixed capacity)
+        rec_bytes = rec_cap * C_SIZEOF_DET
+        send = [torch.empty((B, rec_bytes + 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        recv = ([[torch.empty_like(send[0]) for _ in range(world)] for _ in range(2)] if rank == 0 else [None, None])
+        gwork = [None, None]
+
+    def gather_results(d, s):
+        """Fixed-capacity detection records of this rank's batch -> rank 0 (RCCL gather)."""
+        i = s % 2
+        if gwork[i] is not None:
+            gwork[i].wait()
+        host = np.zeros((B, rec_bytes + 4), np.uint8)
+        raw = np.frombuffer(d._out, dtype=np.uint8).reshape(B, -1)[:, :rec_bytes]
+        host[:, 4:] = raw
+        host[:, :4] = np.array([min(d._n[f], rec_cap) for f in range(B)], np.uint32).view(np.uint8).reshape(B, 4)
+        send[i].copy_(torch.from_numpy(host))
+        gwork[i] = dist.gather(send[i], gather_list=recv[i], dst=0, async_op=True)
 
     def batch_ptr(step):
         off = (step * B) % npool
@@ -143,6 +184,8 @@ def main():
 
     def run(nsteps, step0=0):
         """Round-robin over two detectors: enqueue k, then collect k-1."""
+        if scatter:
+            return run_scatter(nsteps, step0)
         ndet = 0
         prev = None
         for s in range(nsteps):
@@ -153,6 +196,29 @@ def main():
             prev = d
         if prev is not None:
             ndet += sum(prev.collect(counts_only=True))
+        return ndet
+
+    def run_scatter(nsteps, step0):
+        """Scatter of step k+1 overlaps detection of step k (double-buffered)."""
+        ndet = 0
+        prev = None
+        ingest.start(step0)
+        for s in range(nsteps):
+            buf = ingest.ready(step0 + s)
+            d = dets[s % 2]
+            d.enqueue_device(buf.data_ptr(), stride, B)
+            if prev is not None:
+                ndet += sum(prev.collect(counts_only=True))
+                gather_results(prev, step0 + s - 1)
+            prev = d
+            if s + 1 < nsteps:
+                ingest.start(step0 + s + 1)  # its buffer was read by step s-1, collected above
+        if prev is not None:
+            ndet += sum(prev.collect(counts_only=True))
+            gather_results(prev, step0 + nsteps - 1)
+        for w in gwork:
+            if w is not None:
+                w.wait()
         return ndet
 
     run(max(1, args.warmup))
@@ -177,13 +243,13 @@ def main():
         d.set_kernel_timer(dominant)  # reset the accumulators
 
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ndet = run(args.steps, step0=args.warmup)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -224,7 +290,7 @@ def main():
     lat_d = np.array(lat_d or [0.0]) * 1e3
 
     if rank != 0:
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
             dist.destroy_process_group()
         return
@@ -256,7 +322,10 @@ def main():
         "config": {"workload": "configs[1]: 1280x720 single-camera synthetic tag36h11 stream "
                                "(%d tags/frame, YUYV, frames resident in HBM)" % args.tags,
                    "width": W, "height": H, "batch_per_gpu": B, "distinct_frames_per_gpu": npool,
-                   "parallelism": "frame-sharded x%d (no data-path collective)" % world},
+                   "parallelism": ("frame-sharded x%d, frames scattered from rank 0 over RCCL, records gathered "
+                                   "to rank 0" % world) if scatter else
+                                  "frame-sharded x%d (no data-path collective)" % world,
+                   "ingest": "scatter" if scatter else "local"},
         "p50_latency_ms": round(float(np.percentile(lat_h, 50)), 4),
         "p99_latency_ms": round(float(np.percentile(lat_h, 99)), 4),
         "latency_note": "B=1, pageable host YUYV frame -> detections + poses in host memory",
@@ -288,8 +357,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(frames, W, H)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)[:200]}
-    print(json.dumps(out), flush=True)
-    if world > 1:
+    print(json.dumps(out), file=json_out, flush=True)
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -74,6 +74,46 @@ def gather_detections(dist, packed: np.ndarray, device):
     return np.concatenate([g.cpu().numpy() for g in gl], axis=0)
 
 
+class ScatterIngest:
+    """Double-buffered frame ingest from rank 0 (north-star topology).
+
+    Rank 0 holds every rank's frames in device memory; ``start(step)`` launches
+    the scatter of step `step`'s batch (async RCCL/gloo collective) into buffer
+    step % 2, ``ready(step)`` waits for it and returns that buffer.  The caller
+    must have finished reading buffer (step % 2) -- i.e. collected step - 2 --
+    before ``start(step)``.
+    """
+
+    def __init__(self, dist, root_pool, batch: int, frame_shape, device):
+        import torch
+        self.dist, self.batch, self.device = dist, batch, device
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.pool = root_pool  # rank 0: [world, npool, *frame_shape] (None elsewhere)
+        self.npool = int(root_pool.shape[1]) if root_pool is not None else 0
+        self.buf = [torch.empty((batch,) + tuple(frame_shape), dtype=torch.uint8, device=device) for _ in range(2)]
+        self.work = [None, None]
+
+    def _chunks(self, step):
+        if self.rank != 0:
+            return None
+        off = (step * self.batch) % self.npool
+        if off + self.batch > self.npool:
+            off = 0
+        return [self.pool[r, off:off + self.batch] for r in range(self.world)]
+
+    def start(self, step):
+        i = step % 2
+        self.work[i] = self.dist.scatter(self.buf[i], scatter_list=self._chunks(step), src=0, async_op=True)
+
+    def ready(self, step):
+        import torch
+        i = step % 2
+        self.work[i].wait()
+        if self.buf[i].is_cuda:
+            torch.cuda.current_stream(self.buf[i].device).synchronize()  # detector streams are not torch's
+        return self.buf[i]
+
+
 def reduce_max_sum(dist, elapsed: float, count: float, device):
     """(max elapsed over ranks, sum of counts) -- the bench's timing reduction."""
     import torch

@@ -91,3 +91,51 @@ def test_shard_range_covers_all():
                 lo, hi = shard_range(r, world, n)
                 seen.extend(range(lo, hi))
             assert seen == list(range(n))
+
+
+def _ingest_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from ros_vision_amd import multigpu
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, npool, shape = 2, 6, (4, 8)
+    pool = None
+    if rank == 0:  # frame (r, i) is filled with 16*r + i
+        pool = torch.stack([torch.stack([torch.full(shape, 16 * r + i, dtype=torch.uint8) for i in range(npool)])
+                            for r in range(world)])
+    ing = multigpu.ScatterIngest(dist, pool, B, shape, "cpu")
+    got = []
+    ing.start(0)
+    for s in range(5):
+        buf = ing.ready(s)
+        got.append([int(buf[k, 0, 0]) for k in range(B)])
+        if s + 1 < 5:
+            ing.start(s + 1)
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_ingest_double_buffer_world2():
+    """bench.py --ingest scatter: step s delivers rank r the frames (r, s*B mod npool ...)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ingest_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    B, npool = 2, 6
+    for r in range(world):
+        want = []
+        for s in range(5):
+            off = (s * B) % npool
+            want.append([16 * r + off + k for k in range(B)])
+        assert res[r] == want
