@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--tags", type=int, default=15)
     ap.add_argument("--latency-frames", type=int, default=200)
+    ap.add_argument("--instances", type=int, default=2,
+                    help="detector instances (one HIP stream each) used round-robin, i.e. batches in flight")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
     ap.add_argument("--ingest", choices=["local", "scatter"], default="local",
@@ -67,6 +69,8 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
         return 12 * stats.get("large_blob_points", 0)      # 8-B point key + 4 gradient bytes per point
     if kernel == "k_blob_small":
         return 12 * stats.get("small_blob_points", 0)
+    if kernel == "k_extents":  # candidate points read twice, kept points' sort keys written
+        return 24 * (stats.get("small_blob_points", 0) + stats.get("large_blob_points", 0))
     if kernel in ("k_thr_ccl", "k_ccl_final"):
         return nf * 9 * Wd * Hd                            # dec/thr in, labels/sizes out
     return None
@@ -148,7 +152,7 @@ def main():
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
     npool = args.pool
-    dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank) for _ in range(2)]
+    dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank) for _ in range(args.instances)]
     ingest = None
     if scatter:
         # rank 0 holds every rank's frame pool in its HBM; each step scatters B frames per rank
@@ -183,19 +187,21 @@ def main():
         return base + off * stride
 
     def run(nsteps, step0=0):
-        """Round-robin over two detectors: enqueue k, then collect k-1."""
+        """Round-robin over the detector instances: enqueue k, collect k-(instances-1)."""
         if scatter:
             return run_scatter(nsteps, step0)
         ndet = 0
         prev = None
+        ni = len(dets)
+        inflight = []
         for s in range(nsteps):
-            d = dets[s % 2]
+            d = dets[s % ni]
             d.enqueue_device(batch_ptr(step0 + s), stride, B)
-            if prev is not None:
-                ndet += sum(prev.collect(counts_only=True))
-            prev = d
-        if prev is not None:
-            ndet += sum(prev.collect(counts_only=True))
+            inflight.append(d)
+            if len(inflight) == ni:
+                ndet += sum(inflight.pop(0).collect(counts_only=True))
+        for d in inflight:
+            ndet += sum(d.collect(counts_only=True))
         return ndet
 
     def run_scatter(nsteps, step0):

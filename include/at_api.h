@@ -59,7 +59,7 @@ typedef struct {
   float max_line_fit_mse;     /* 10.0 */
   double cos_critical_rad;    /* cos(10 deg) */
   int device;                 /* HIP device ordinal */
-  int max_batch;              /* frames per at_detect_batch / at_detect_device call */
+  int max_batch;              /* frames per at_detect_batch / at_detect_device call (1..256) */
   double tag_size;            /* metres; > 0 also estimates every tag's pose on the GPU
                                  (info_.tagsize = TAGSIZE 0.1651, apriltags_cuda_detector.cu:185,
                                  apriltags_cuda_detector.hpp:39); 0 = detection only */

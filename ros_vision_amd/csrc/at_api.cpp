@@ -37,6 +37,12 @@ static const int kTag36h11Known = (int)(sizeof(kTag36h11) / sizeof(kTag36h11[0])
 
 using namespace at;
 
+// control block layout (u32 words, zeroed every batch): per-frame arrays of B
+// words, then scalars
+enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlPerFrame };
+enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
+       kCtlScalars = kCtlNcls + kNumCls };
+
 struct at_detector {
   at_config cfg;
   at_camera cam;
@@ -166,7 +172,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   const int W = cfg->width, H = cfg->height;
   // GpuDetector preconditions (apriltag_gpu.cu:166-167, 754-755, 774; line_fit_filter.cu:1205)
   if (W <= 16 || H <= 16 || W % 8 || H % 8 || (long)W * H >= (1L << 22)) return AT_E_INVALID;
-  if (cfg->quad_decimate != 2.0f || cfg->max_nmaxima != 10 || cfg->max_batch < 1) return AT_E_INVALID;
+  if (cfg->quad_decimate != 2.0f || cfg->max_nmaxima != 10 || cfg->max_batch < 1 || cfg->max_batch > kMaxBatch)
+    return AT_E_INVALID;
   if (2 * (W + H) > kSortCap) return AT_E_INVALID;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AT_E_HIP;
@@ -196,6 +203,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
+  p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) return AT_E_INVALID;
   p.tag_size = cfg->tag_size;
@@ -207,7 +215,11 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipSetDevice(d->device) != hipSuccess) return fail(AT_E_HIP);
   if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
-  if (hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
+  // AT_NO_FORK=1: the two blob kernels run back to back on the one stream (more
+  // detector instances can then share the process's hardware queues)
+  if (!(getenv("AT_NO_FORK") && atoi(getenv("AT_NO_FORK"))) &&
+      hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess)
+    return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   d->kt.stage = -1;
@@ -252,37 +264,30 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.pair_cnt = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.pair_off = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.pair_sel = (uint32_t*)dalloc(B * kMaxPairs * 4);
-  b.work = (uint32_t*)dalloc(B * kMaxPairs * 4);
-  b.work_small = (uint32_t*)dalloc(B * kMaxPairs * 4);
+  b.wcap = (uint32_t)(B * kMaxPairs);
+  b.work = (uint32_t*)dalloc((size_t)kNumCls * B * kMaxPairs * 4);
   b.probe = (uint64_t*)dalloc(kProbeWords * 8);
   b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
-  b.quads = (QuadRecord*)dalloc(B * kMaxQuads * sizeof(QuadRecord));
-  d->ctrl_words = 6 * B + 8;
+  b.quads = (QuadRecord*)dalloc(B * kMaxPairs * sizeof(QuadRecord));
+  d->ctrl_words = kCtlPerFrame * B + kCtlScalars;
   d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
-  b.npts = d->d_ctrl;
-  b.npairs = d->d_ctrl + B;
-  b.ndets = d->d_ctrl + 2 * B;
-  b.nquads = d->d_ctrl + 3 * B;
-  b.status = d->d_ctrl + 4 * B;
-  b.nwork = d->d_ctrl + 5 * B;
-  b.workhead = d->d_ctrl + 5 * B + 1;
-  b.nqcand = d->d_ctrl + 5 * B + 2;
-  b.qhead = d->d_ctrl + 5 * B + 3;
-  b.npent = d->d_ctrl + 5 * B + 4;
-  b.blob_pts = d->d_ctrl + 6 * B + 6;
-  b.nwork_small = d->d_ctrl + 6 * B + 4;
-  b.workhead_small = d->d_ctrl + 6 * B + 5;
+  b.npts = d->d_ctrl + kCtlNpts * B;
+  b.npairs = d->d_ctrl + kCtlNpairs * B;
+  b.ndets = d->d_ctrl + kCtlNdets * B;
+  b.nquads = d->d_ctrl + kCtlNquads * B;
+  b.status = d->d_ctrl + kCtlStatus * B;
+  b.npent = d->d_ctrl + kCtlNpent * B;
+  b.nqcand = d->d_ctrl + kCtlNqcand * B;
+  uint32_t* sc = d->d_ctrl + kCtlPerFrame * B;
+  b.workhead = sc + kCtlWorkhead;
+  b.qhead = sc + kCtlQhead;
+  b.workhead_small = sc + kCtlWorkheadSmall;
+  b.blob_pts = sc + kCtlBlobPts;
+  b.ncls = sc + kCtlNcls;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
-  // blob scratch: large teams (nblobwg x kSortCap) and small teams (8 x nblobwg x kSmallBlob),
-  // disjoint because the two kernels run concurrently
-  const size_t nl = (size_t)d->nblobwg * kSortCap, ns = (size_t)d->nblobwg * 8 * kSmallBlob;
-  b.s_i32 = (int32_t*)dalloc(nl * 3 * 4);
-  b.s_i64 = (int64_t*)dalloc(nl * 3 * 8);
-  b.s_f64 = (double*)dalloc(nl * 2 * 8);
-  b.ss_i32 = (int32_t*)dalloc(ns * 3 * 4);
-  b.ss_i64 = (int64_t*)dalloc(ns * 3 * 8);
-  b.ss_f64 = (double*)dalloc(ns * 2 * 8);
+  // overflow area for the peak keys of pathological large blobs (one per large-blob team)
+  b.s_pk = (uint64_t*)dalloc((size_t)d->nblobwg * (kSortCap / 2) * 8);
   if (oom) return fail(AT_E_NOMEM);
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
   d->poses.assign(B * kMaxDets, at_pose{});
@@ -453,8 +458,8 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   const int B = d->B;
   int rc = AT_OK;
   for (int f = 0; f < d->last_nframes; f++) {
-    const uint32_t status = d->h_ctrl[4 * B + f];
-    const int ncand = (int)std::min<uint32_t>(d->h_ctrl[2 * B + f], (uint32_t)kMaxDets);
+    const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
+    const int ncand = (int)std::min<uint32_t>(d->h_ctrl[kCtlNdets * B + f], (uint32_t)kMaxDets);
     int n = 0;
     if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow)) {
       rc = AT_E_CAPACITY;
@@ -568,13 +573,13 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   uint64_t v[8] = {0};
   v[0] = (uint64_t)d->last_nframes;
   for (int f = 0; f < d->last_nframes; f++) {
-    v[1] += d->h_ctrl[f];
-    v[2] += d->h_ctrl[B + f];
-    v[5] += d->h_ctrl[3 * B + f];
-    v[6] += d->h_ctrl[2 * B + f];
+    v[1] += d->h_ctrl[kCtlNpts * B + f];
+    v[2] += d->h_ctrl[kCtlNpairs * B + f];
+    v[5] += d->h_ctrl[kCtlNquads * B + f];
+    v[6] += d->h_ctrl[kCtlNdets * B + f];
   }
-  v[3] = d->h_ctrl[6 * B + 6];
-  v[4] = d->h_ctrl[6 * B + 7];
+  v[3] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts];
+  v[4] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts + 1];
   const int n = std::min(cap, 7);
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
@@ -612,7 +617,7 @@ int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const d
 
 int at_frame_status(at_detector* d, int frame) {
   if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
-  const uint32_t s = d->h_ctrl[4 * d->B + frame];
+  const uint32_t s = d->h_ctrl[kCtlStatus * d->B + frame];
   return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow))
              ? AT_E_CAPACITY
              : AT_OK;
@@ -636,24 +641,31 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
     case AT_STAGE_SIZES: src = d->d.size + frame * nd; n = nd * 4; break;
     case AT_STAGE_NUM_POINTS:
       if (bytes < 4) return AT_E_INVALID;
-      memcpy(dst, &d->h_ctrl[frame], 4);
+      memcpy(dst, &d->h_ctrl[kCtlNpts * B + frame], 4);
       return 4;
     case AT_STAGE_NUM_PAIRS:
       if (bytes < 4) return AT_E_INVALID;
-      memcpy(dst, &d->h_ctrl[B + frame], 4);
+      memcpy(dst, &d->h_ctrl[kCtlNpairs * B + frame], 4);
       return 4;
     case AT_STAGE_NUM_PAIR_ENTRIES:
       if (bytes < 4) return AT_E_INVALID;
-      memcpy(dst, &d->h_ctrl[5 * B + 4 + frame], 4);
+      memcpy(dst, &d->h_ctrl[kCtlNpent * B + frame], 4);
       return 4;
     case AT_STAGE_PROBE: src = d->d.probe; n = kProbeWords * 8; break;
     case AT_STAGE_QUADS: {
-      const uint32_t nq = std::min<uint32_t>(d->h_ctrl[3 * B + frame], (uint32_t)kMaxQuads);
-      std::vector<QuadRecord> q(nq);
-      if (nq && hipMemcpy(q.data(), d->d.quads + (size_t)frame * kMaxQuads, nq * sizeof(QuadRecord),
-                          hipMemcpyDeviceToHost) != hipSuccess)
+      // one record per kept blob, in the slot of its pair rank (pair_sel marks them)
+      const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[kCtlNpairs * B + frame], (uint32_t)kMaxPairs);
+      std::vector<QuadRecord> all(npairs);
+      std::vector<uint32_t> sel(npairs);
+      if (npairs && (hipMemcpy(all.data(), d->d.quads + (size_t)frame * kMaxPairs, npairs * sizeof(QuadRecord),
+                               hipMemcpyDeviceToHost) != hipSuccess ||
+                     hipMemcpy(sel.data(), d->d.pair_sel + (size_t)frame * kMaxPairs, npairs * 4,
+                               hipMemcpyDeviceToHost) != hipSuccess))
         return AT_E_HIP;
-      std::sort(q.begin(), q.end(), [](const QuadRecord& a, const QuadRecord& b) { return a.blob_index < b.blob_index; });
+      std::vector<QuadRecord> q;
+      for (uint32_t i = 0; i < npairs; i++)
+        if (sel[i]) q.push_back(all[i]);
+      const uint32_t nq = (uint32_t)q.size();
       const size_t need = nq * sizeof(at_quad_record);
       if (bytes < need) return AT_E_INVALID;
       for (uint32_t i = 0; i < nq; i++) {
@@ -668,14 +680,14 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       return (long long)need;
     }
     case AT_STAGE_POINTS: {
-      const uint32_t np = std::min<uint32_t>(d->h_ctrl[frame], (uint32_t)g.cap_pts);
+      const uint32_t np = std::min<uint32_t>(d->h_ctrl[kCtlNpts * B + frame], (uint32_t)g.cap_pts);
       src = d->d.pts + (size_t)frame * g.cap_pts;
       n = (size_t)np * 8;
       break;
     }
     case AT_STAGE_BLOB_POINTS: {
       // IndexPoint keys of the selected pairs, in rank order
-      const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[B + frame], (uint32_t)kMaxPairs);
+      const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[kCtlNpairs * B + frame], (uint32_t)kMaxPairs);
       std::vector<uint32_t> cnt(npairs), off(npairs), sel(npairs);
       if (npairs) {
         if (hipMemcpy(cnt.data(), d->d.pair_cnt + (size_t)frame * kMaxPairs, npairs * 4, hipMemcpyDeviceToHost) ||

@@ -15,22 +15,26 @@ constexpr int kHashBits = 13;
 constexpr int kPairEntCap = 65536;     // per-frame (tile, pair, count) entries k_boundary hands to k_pairs
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kMaxDets = 128;          // candidate detections per frame
-constexpr int kMaxQuads = 2048;        // fitted-quad debug records per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
-// Blobs of more than kSmallBlob points: one workgroup each, 1024 threads for
+// Blobs of more than kSmallBlob points: one workgroup each, 512 threads for
 // small batches (latency: the biggest blob is the critical path), 256 for
 // large batches (throughput: more blobs in flight per CU).
 constexpr int kWideBlobMaxBatch = 8;
 constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wave-per-blob
-constexpr int kLdsBlob = 256;          // ... and keep their prefix moments / errors in LDS up to this many
 constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
-constexpr int kNumStages = 11;
-constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final", "k_boundary",
-                                                 "k_pairs", "k_group",   "k_blob_small", "k_blob",       "k_decode",
-                                                 "k_pose"};
+constexpr int kNumStages = 12;
+constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final",
+                                                 "k_boundary", "k_pairs", "k_group",     "k_extents",
+                                                 "k_blob_small", "k_blob", "k_decode",   "k_pose"};
+
+// ---- blob size classes of the work lists, processed largest first ----------
+// 0-2: large blobs (> kSmallBlob points, workgroup per blob), 3-6: small blobs
+// (wave per blob).  Longest-first order shortens the persistent kernels' tail.
+constexpr int kNumCls = 7;
+constexpr int kNumLargeCls = 3;
 
 // ---- per-frame status bits -------------------------------------------------
 constexpr uint32_t kStatusPairsOverflow = 1u;   // N_q > kMaxPairs
@@ -38,6 +42,7 @@ constexpr uint32_t kStatusHashFull = 2u;
 constexpr uint32_t kStatusDetsOverflow = 4u;
 constexpr uint32_t kStatusPointsOverflow = 8u;
 constexpr uint32_t kStatusQuadsOverflow = 16u;
+constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config.max_batch)
 constexpr int kQuadCandPerFrame = 512;  // accepted quads queued for decode, per frame of the batch
 
 // Frame geometry (all derived from W, H).
@@ -62,6 +67,7 @@ struct Params {
   int diag_stop;  // diagnostics only (AT_DIAG_BLOB_STOP): k_blob returns after phase N; 0 = full
   double tag_size;  // metres; > 0 runs k_pose (apriltags_cuda_detector.hpp:39 TAGSIZE)
   int probe;      // diagnostics only (AT_PHASE_PROBE): kernels stamp phase clocks into DevBufs::probe
+  int taps;       // write the sorted IndexPoint parity tap (AT_STAGE_BLOB_POINTS) over the grouped points
 };
 constexpr int kProbeWords = 256;
 
@@ -120,33 +126,28 @@ struct DevBufs {
   uint32_t* pair_cnt; // [B][kMaxPairs]
   uint32_t* pair_off; // [B][kMaxPairs]
   uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair
-  uint32_t* work;     // [B*kMaxPairs]   (frame << 16) | rank of candidate pairs (> kSmallBlob points)
-  uint32_t* work_small; // [B*kMaxPairs] same, <= kSmallBlob points
+  uint32_t* work;     // [kNumCls][wcap] (frame << 16) | rank of candidate pairs, by size class
+  uint32_t wcap;      // B * kMaxPairs
   DevDetection* dets; // [B][kMaxDets]
-  QuadRecord* quads;  // [B][kMaxQuads]
+  QuadRecord* quads;  // [B][kMaxPairs]  fitted-quad debug record of each kept blob, slot = pair rank
   // control block (zeroed every batch)
   uint32_t* npts;     // [B]
   uint32_t* npairs;   // [B]
   uint32_t* ndets;    // [B]
   uint32_t* nquads;   // [B]
   uint32_t* status;   // [B]
-  uint32_t* nwork;    // [1]
+  uint32_t* ncls;     // [kNumCls] candidate pairs per size class
   uint32_t* workhead; // [1]
   uint64_t* probe;    // [kProbeWords] phase clock stamps (diagnostics)
   uint32_t* blob_pts;       // [2] points processed by the small / large blob kernels (batch statistics)
-  uint32_t* nwork_small;    // [1]
   uint32_t* workhead_small; // [1]
-  uint32_t* nqcand;   // [1]
+  uint32_t* nqcand;   // [B] accepted quads queued for decode, per frame (qcand[f][kQuadCandPerFrame])
   uint32_t* qhead;    // [1]
   QuadCand* qcand;    // [qcand_cap]
   uint32_t qcand_cap;
   // per-workgroup scratch of the blob kernel
-  int32_t* s_i32;     // [nblobwg][3][kSortCap]  prefix Mx, My, W        (large-blob teams)
-  int64_t* s_i64;     // [nblobwg][3][kSortCap]  prefix Mxx, Myy, Mxy
-  double* s_f64;      // [nblobwg][2][kSortCap]  errs, filtered errs
-  int32_t* ss_i32;    // [8*nblobwg][3][kSmallBlob] the same for the small-blob teams, which
-  int64_t* ss_i64;    // run concurrently with the large ones (separate regions)
-  double* ss_f64;
+  uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
+                      // (pathological blobs only; every other per-blob array lives in LDS)
 };
 
 }  // namespace at

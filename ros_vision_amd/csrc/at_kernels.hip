@@ -26,9 +26,6 @@
 #include "at_common.h"
 #include "at_pose.h"
 
-#ifndef AT_LDS_BLOB
-#define AT_LDS_BLOB 0  // small-blob prefix moments in LDS (trades occupancy for latency)
-#endif
 
 namespace at {
 
@@ -137,20 +134,24 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
 // "link to the smaller slot" == "link to the smaller id" and every local root
 // is the minimum node id of its local component.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lds_find(volatile uint32_t* par, uint32_t n) {
-  uint32_t p = par[n];
+// (relaxed atomic loads, not volatile: a volatile access through the generic
+// pointer would be compiled to flat instructions instead of ds_read)
+__device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_find(uint32_t* par, uint32_t n) {
+  uint32_t p = lds_load(par + n);
   while (p != n) {
     n = p;
-    p = par[n];
+    p = lds_load(par + n);
   }
   return n;
 }
 
-__device__ void lds_union(uint32_t* par, uint32_t a, uint32_t b) {
-  volatile uint32_t* vp = par;
+__device__ __forceinline__ void lds_union(uint32_t* par, uint32_t a, uint32_t b) {
   while (true) {
-    a = lds_find(vp, a);
-    b = lds_find(vp, b);
+    a = lds_find(par, a);
+    b = lds_find(par, b);
     if (a == b) return;
     if (a < b) {
       const uint32_t old = atomicMin(&par[b], a);
@@ -509,6 +510,9 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
   __shared__ uint64_t s_pts[kBndPts];
   __shared__ uint32_t s_npts, s_nent, s_base, s_ebase;
+  __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
+  __shared__ uint8_t s_tbig[(4 * kBndRows + 1) * 66];
+  __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
   const int f = blockIdx.z;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   for (int i = tid; i < kLdsPairSlots; i += 256) {
@@ -516,33 +520,59 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
     s_pcnt[i] = 0;
   }
   if (tid == 0) { s_npts = 0; s_nent = 0; }
-  __syncthreads();  // LDS table initialised
-  const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+  // stage the tile's threshold values and labels (+1 halo: rows y0..y0+16, cols
+  // x0-1..x0+64) and, per pixel, whether its blob has >= 25 pixels: two
+  // dependent global round trips per workgroup, then the point logic runs on LDS
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   const uint8_t* thr = b.thr + fo;
   const uint32_t* lab = b.lab + fo;
   const uint32_t* size = b.size + fo;
   const int Wd = g.Wd;
+  const int ty0 = 1 + blockIdx.y * (4 * kBndRows), tx0 = blockIdx.x * 64;  // halo origin: x0 - 1
+  constexpr int kTR = 4 * kBndRows + 1, kTC = 66, kTN = kTR * kTC;
+  constexpr int kPer = (kTN + 255) / 256;
+  uint32_t lv[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int e = tid + 256 * k;
+    const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
+    lv[k] = 0xffffffffu;
+    if (e < kTN && yy < g.Hd && xx < Wd) {
+      const size_t i = (size_t)yy * Wd + xx;
+      const uint32_t v = thr[i];
+      s_tthr[e] = (uint8_t)v;
+      if (v != 127) lv[k] = lab[i];
+    } else if (e < kTN) {
+      s_tthr[e] = 127;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int e = tid + 256 * k;
+    if (e < kTN) {
+      s_tlab[e] = lv[k];
+      s_tbig[e] = lv[k] != 0xffffffffu && size[lv[k]] >= 25;
+    }
+  }
+  __syncthreads();  // LDS tables initialised
+  const int x = 1 + blockIdx.x * 64 + threadIdx.x;
   const uint32_t lane = lane_id();
   for (int r = 0; r < kBndRows; r++) {
-    const int y = 1 + (blockIdx.y * kBndRows + r) * 4 + threadIdx.y;
+    const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
+    const int y = ty0 + ly;
     uint64_t pk[4] = {0, 0, 0, 0};
     if (x <= g.Wd - 2 && y <= g.Hd - 2) {
-      const size_t i0 = (size_t)y * Wd + x;
-      const uint8_t v0 = thr[i0];
-      if (v0 != 127) {
-        const uint32_t rep0 = lab[i0];
-        if (size[rep0] >= 25) {
-          const uint8_t vr = thr[i0 + 1], vd = thr[i0 + Wd], vdr = thr[i0 + Wd + 1], vdl = thr[i0 + Wd - 1],
-                        vl = thr[i0 - 1];
-          const uint32_t lr = lab[i0 + 1], ld = lab[i0 + Wd], ldr = lab[i0 + Wd + 1], ldl = lab[i0 + Wd - 1],
-                         ll = lab[i0 - 1];
-          if (v0 + vr == 255 && size[lr] >= 25) pk[0] = make_qbp(rep0, lr, x, y, 0, vr > v0);
-          if (v0 + vdr == 255 && size[ldr] >= 25) pk[1] = make_qbp(rep0, ldr, x, y, 1, vdr > v0);
-          if (v0 + vd == 255 && size[ld] >= 25) pk[2] = make_qbp(rep0, ld, x, y, 2, vd > v0);
-          const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && size[ll] >= 25 && size[ld] >= 25;
-          if (!dedup && v0 + vdl == 255 && size[ldl] >= 25) pk[3] = make_qbp(rep0, ldl, x, y, 3, vdl > v0);
-        }
+      const int e0 = ly * kTC + threadIdx.x + 1;
+      const uint8_t v0 = s_tthr[e0];
+      if (v0 != 127 && s_tbig[e0]) {
+        const uint32_t rep0 = s_tlab[e0];
+        const int er = e0 + 1, ed = e0 + kTC, edr = ed + 1, edl = ed - 1, el = e0 - 1;
+        const uint8_t vr = s_tthr[er], vd = s_tthr[ed], vdr = s_tthr[edr], vdl = s_tthr[edl], vl = s_tthr[el];
+        if (v0 + vr == 255 && s_tbig[er]) pk[0] = make_qbp(rep0, s_tlab[er], x, y, 0, vr > v0);
+        if (v0 + vdr == 255 && s_tbig[edr]) pk[1] = make_qbp(rep0, s_tlab[edr], x, y, 1, vdr > v0);
+        if (v0 + vd == 255 && s_tbig[ed]) pk[2] = make_qbp(rep0, s_tlab[ed], x, y, 2, vd > v0);
+        const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && s_tbig[el] && s_tbig[ed];
+        if (!dedup && v0 + vdl == 255 && s_tbig[edl]) pk[3] = make_qbp(rep0, s_tlab[edl], x, y, 3, vdl > v0);
       }
     }
     uint32_t npk = 0;
@@ -616,6 +646,16 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
 // pairs whose point count passes the size filter to the global work list.
 // One 1024-thread workgroup per frame; bitonic sort in LDS.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int size_class(uint32_t n) {
+  if (n > 2048) return 0;
+  if (n > 1024) return 1;
+  if (n > (uint32_t)kSmallBlob) return 2;
+  if (n > 256) return 3;
+  if (n > 128) return 4;
+  if (n > 64) return 5;
+  return 6;
+}
+
 template <typename T, int NT>
 __device__ void block_bitonic_sort(T* s, int n) {
   for (int k = 2; k <= n; k <<= 1) {
@@ -745,37 +785,26 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const uint32_t offs[4] = {excl, excl + c0, excl + c0 + c1, excl + c0 + c1 + c2};
   const uint32_t cs[4] = {c0, c1, c2, c3};
   stamp(4);
-  // work-list appends: one global atomic per list per workgroup
-  bool take[4], small[4];
-  uint32_t nsl = 0;
+  // work-list appends by size class: LDS slots, then one global atomic per
+  // class per workgroup
+  __shared__ uint32_t s_ccnt[kNumCls], s_cbase[kNumCls];
+  __syncthreads();  // s_n / s_full / s_wsum reads done
+  if (tid < kNumCls) s_ccnt[tid] = 0;
+  __syncthreads();
+  int cls[4];
+  uint32_t lslot[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    take[k] = i0 + k < (int)n && cs[k] >= g.min_cluster && cs[k] <= g.max_cluster;
-    small[k] = cs[k] <= (uint32_t)kSmallBlob;
-    nsl += take[k] ? (small[k] ? 1u : 0x10000u) : 0u;
-  }
-  uint32_t winc = nsl;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(winc, d);
-    if (lane >= (uint32_t)d) winc += v;
-  }
-  __syncthreads();  // s_wsum reuse
-  if (lane == 63) s_wsum[tid >> 6] = winc;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t tot = 0;
-    for (int w = 0; w < 16; w++) {
-      const uint32_t t = s_wsum[w];
-      s_wsum[w] = tot;
-      tot += t;
+    cls[k] = -1;
+    lslot[k] = 0;
+    if (i0 + k < (int)n && cs[k] >= g.min_cluster && cs[k] <= g.max_cluster) {
+      cls[k] = size_class(cs[k]);
+      lslot[k] = atomicAdd(&s_ccnt[cls[k]], 1u);
     }
-    s_n = (tot & 0xffff) ? atomicAdd(b.nwork_small, tot & 0xffff) : 0u;
-    s_full = (tot >> 16) ? atomicAdd(b.nwork, tot >> 16) : 0u;
   }
   __syncthreads();
-  const uint32_t wpre = s_wsum[tid >> 6] + winc - nsl;
-  uint32_t ps = s_n + (wpre & 0xffff), pl = s_full + (wpre >> 16);
+  if (tid < kNumCls) s_cbase[tid] = s_ccnt[tid] ? atomicAdd(b.ncls + tid, s_ccnt[tid]) : 0u;
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
@@ -787,10 +816,8 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
       b.pair_off[(size_t)f * kMaxPairs + i] = offs[k];
       b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
-      if (take[k]) {
-        if (small[k]) b.work_small[ps++] = ((uint32_t)f << 16) | (uint32_t)i;
-        else b.work[pl++] = ((uint32_t)f << 16) | (uint32_t)i;
-      }
+      if (cls[k] >= 0)
+        b.work[(size_t)cls[k] * b.wcap + s_cbase[cls[k]] + lslot[k]] = ((uint32_t)f << 16) | (uint32_t)i;
     }
   }
   stamp(5);
@@ -857,37 +884,6 @@ struct Moments {
   int64_t Mxx, Myy, Mxy;
   int32_t N;
 };
-
-struct BlobScratch {
-  int32_t *Mx, *My, *W;
-  int64_t *Mxx, *Myy, *Mxy;
-  double *err, *filt;
-};
-
-__device__ __forceinline__ Moments read_moments(const BlobScratch& P, uint32_t n, uint32_t i0, uint32_t i1) {
-  Moments m;
-  if (i0 < i1) {
-    m.N = (int32_t)(i1 - i0 + 1);
-    m.Mx = P.Mx[i1]; m.My = P.My[i1]; m.W = P.W[i1];
-    m.Mxx = P.Mxx[i1]; m.Myy = P.Myy[i1]; m.Mxy = P.Mxy[i1];
-    if (i0 > 0) {
-      m.Mx = (int32_t)((uint32_t)m.Mx - (uint32_t)P.Mx[i0 - 1]);
-      m.My = (int32_t)((uint32_t)m.My - (uint32_t)P.My[i0 - 1]);
-      m.W = (int32_t)((uint32_t)m.W - (uint32_t)P.W[i0 - 1]);
-      m.Mxx -= P.Mxx[i0 - 1]; m.Myy -= P.Myy[i0 - 1]; m.Mxy -= P.Mxy[i0 - 1];
-    }
-  } else {
-    const uint32_t a = i0 - 1, z = n - 1;
-    m.Mx = (int32_t)((uint32_t)P.Mx[z] - (uint32_t)P.Mx[a] + (uint32_t)P.Mx[i1]);
-    m.My = (int32_t)((uint32_t)P.My[z] - (uint32_t)P.My[a] + (uint32_t)P.My[i1]);
-    m.W = (int32_t)((uint32_t)P.W[z] - (uint32_t)P.W[a] + (uint32_t)P.W[i1]);
-    m.Mxx = P.Mxx[z] - P.Mxx[a] + P.Mxx[i1];
-    m.Myy = P.Myy[z] - P.Myy[a] + P.Myy[i1];
-    m.Mxy = P.Mxy[z] - P.Mxy[a] + P.Mxy[i1];
-    m.N = (int32_t)(n - i0 + i1 + 1);
-  }
-  return m;
-}
 
 // FitLine (line_fit_filter.cu:798-872) / HostFitLine (apriltag_detect.cu:38-90)
 __device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* err, double* mse) {
@@ -1071,43 +1067,77 @@ __device__ void hproject(const double* H, double x, double y, double* ox, double
   *oy = yy / zz;
 }
 
-__device__ int homography_compute2(const double c[4][4], double* H) {
-  double A[72];
-  for (int i = 0; i < 4; i++) {
-    double* r0 = &A[(2 * i) * 9];
-    double* r1 = &A[(2 * i + 1) * 9];
-    r0[0] = c[i][0]; r0[1] = c[i][1]; r0[2] = 1; r0[3] = 0; r0[4] = 0; r0[5] = 0;
-    r0[6] = -c[i][0] * c[i][2]; r0[7] = -c[i][1] * c[i][2]; r0[8] = c[i][2];
-    r1[0] = 0; r1[1] = 0; r1[2] = 0; r1[3] = c[i][0]; r1[4] = c[i][1]; r1[5] = 1;
-    r1[6] = -c[i][0] * c[i][3]; r1[7] = -c[i][1] * c[i][3]; r1[8] = c[i][3];
+// homography_compute2 (apriltag 3.x common/homography.c) for the 8x9 DLT system
+// held in LDS (A[8][9]), spread over one wave: pivot search (first maximum,
+// strict >, rows col..7), row swap and elimination in parallel.  Every element
+// goes through exactly the serial sequence of operations (fct = A[i][col] /
+// A[col][col]; A[i][j] -= fct * A[col][j]), so the result is bit-identical to
+// the one-lane restatement (oracle/ao_oracle.c homography_compute2).  The
+// eliminated sub-diagonal entries are never read again and are not zeroed.
+// Returns 0 / -1 (singular), uniform across the wave; H valid on every lane.
+__device__ int homography_wave(const float (*qc)[2], double* A, double* H) {
+  const int lane = (int)lane_id();
+  for (int e = lane; e < 72; e += 64) {
+    const int row = e / 9, col = e % 9, i = row >> 1;
+    const double c0 = (i == 0 || i == 3) ? -1 : 1, c1 = (i == 0 || i == 1) ? -1 : 1;
+    const double c2 = qc[i][0], c3 = qc[i][1];
+    // row 2i: (c0, c1, 1, 0, 0, 0, -c0 c2, -c1 c2, c2); row 2i+1: (0, 0, 0, c0, c1, 1, -c0 c3, -c1 c3, c3)
+    const int k = (row & 1) ? col - 3 : col;  // position inside the (c0, c1, 1) triple
+    const double cz = (row & 1) ? c3 : c2;
+    double v = 0;
+    if (k == 0) v = c0;
+    else if (k == 1) v = c1;
+    else if (k == 2) v = 1;
+    if (col == 6) v = -c0 * cz;
+    else if (col == 7) v = -c1 * cz;
+    else if (col == 8) v = cz;
+    A[e] = v;
   }
+  __syncthreads();
   for (int col = 0; col < 8; col++) {
-    double max_val = 0;
-    int max_idx = -1;
-    for (int row = col; row < 8; row++) {
-      const double v = fabs(A[row * 9 + col]);
-      if (v > max_val) { max_val = v; max_idx = row; }
+    // pivot: first row (col..7) holding the strict maximum of |A[row][col]| > 0
+    double v = -1.0;
+    int row = 64;
+    if (lane < 8 - col) {
+      row = col + lane;
+      v = fabs(A[row * 9 + col]);
+      if (!(v > 0.0)) { v = -1.0; row = 64; }  // NaN and 0 never win the serial strict '>'
     }
-    if (max_val < 1e-10) return -1;
-    if (max_idx != col)
-      for (int i = col; i < 9; i++) {
-        const double t = A[col * 9 + i];
-        A[col * 9 + i] = A[max_idx * 9 + i];
-        A[max_idx * 9 + i] = t;
-      }
-    for (int i = col + 1; i < 8; i++) {
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+      const double ov = __shfl_xor(v, d);
+      const int orow = __shfl_xor(row, d);
+      if (ov > v || (ov == v && orow < row)) { v = ov; row = orow; }
+    }
+    v = __shfl(v, 0);
+    row = __shfl(row, 0);
+    if (!(v >= 1e-10)) return -1;  // max_val < 1e-10 (max_val starts at 0)
+    if (row != col && lane <= 8 - col) {
+      const int i = col + lane;
+      const double t = A[col * 9 + i];
+      A[col * 9 + i] = A[row * 9 + i];
+      A[row * 9 + i] = t;
+    }
+    __syncthreads();
+    const int nc = 8 - col;  // columns col+1..8
+    if (lane < (7 - col) * nc) {
+      const int i = col + 1 + lane / nc, j = col + 1 + lane % nc;
       const double fct = A[i * 9 + col] / A[col * 9 + col];
-      A[i * 9 + col] = 0;
-      for (int j = col + 1; j < 9; j++) A[i * 9 + j] -= fct * A[col * 9 + j];
+      A[i * 9 + j] -= fct * A[col * 9 + j];
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    for (int col = 7; col >= 0; col--) {
+      double sum = 0;
+      for (int i = col + 1; i < 8; i++) sum += A[col * 9 + i] * A[i * 9 + 8];
+      A[col * 9 + 8] = (A[col * 9 + 8] - sum) / A[col * 9 + col];
     }
   }
-  for (int col = 7; col >= 0; col--) {
-    double sum = 0;
-    for (int i = col + 1; i < 8; i++) sum += A[col * 9 + i] * A[i * 9 + 8];
-    A[col * 9 + 8] = (A[col * 9 + 8] - sum) / A[col * 9 + col];
-  }
-  H[0] = A[8]; H[1] = A[17]; H[2] = A[26]; H[3] = A[35]; H[4] = A[44]; H[5] = A[53];
-  H[6] = A[62]; H[7] = A[71]; H[8] = 1;
+  __syncthreads();
+  if (lane < 8) H[lane] = A[lane * 9 + 8];
+  if (lane == 8) H[8] = 1;
+  __syncthreads();
   return 0;
 }
 
@@ -1158,24 +1188,118 @@ __device__ __forceinline__ LineFitOut fit_line_v(const Moments& m) {
   return o;
 }
 
+// Moments of a run of line-fit points (LineFitPoint, line_fit_filter.h:61-83) in
+// the reference's integer widths: Mx, My, W wrap as int32 and Mxx, Myy, Mxy as
+// int64 (kept here as u32 / u64 so wrapping is defined).  Sums, differences and
+// prefix differences are then exact modulo 2^32 / 2^64, which is what the
+// reference's int32 / int64 prefix sums compute.
+struct Mom6 {
+  uint32_t Mx, My, W;
+  uint64_t Mxx, Myy, Mxy;
+};
+__device__ __forceinline__ Mom6 mom_zero() { return Mom6{0, 0, 0, 0, 0, 0}; }
+__device__ __forceinline__ void mom_add(Mom6& a, const Mom6& c) {
+  a.Mx += c.Mx; a.My += c.My; a.W += c.W; a.Mxx += c.Mxx; a.Myy += c.Myy; a.Mxy += c.Mxy;
+}
+__device__ __forceinline__ void mom_sub(Mom6& a, const Mom6& c) {
+  a.Mx -= c.Mx; a.My -= c.My; a.W -= c.W; a.Mxx -= c.Mxx; a.Myy -= c.Myy; a.Mxy -= c.Mxy;
+}
+__device__ __forceinline__ Mom6 mom_shfl(const Mom6& m, int src) {
+  Mom6 r;
+  r.Mx = __shfl(m.Mx, src); r.My = __shfl(m.My, src); r.W = __shfl(m.W, src);
+  r.Mxx = __shfl(m.Mxx, src); r.Myy = __shfl(m.Myy, src); r.Mxy = __shfl(m.Mxy, src);
+  return r;
+}
+__device__ __forceinline__ Mom6 mom_shfl_up(const Mom6& m, int d) {
+  Mom6 r;
+  r.Mx = __shfl_up(m.Mx, d); r.My = __shfl_up(m.My, d); r.W = __shfl_up(m.W, d);
+  r.Mxx = __shfl_up(m.Mxx, d); r.Myy = __shfl_up(m.Myy, d); r.Mxy = __shfl_up(m.Mxy, d);
+  return r;
+}
+
+// Compact point word of a sorted blob point: bx [9:0], by [19:10], dxy [21:20],
+// W [30:22] (W = (int)(hypotf(gx, gy) + 1) <= 361).
+__device__ __forceinline__ uint32_t compact_word(uint64_t sk, int32_t Wt) {
+  return (uint32_t)((sk >> 1) & 0x3ff) | ((uint32_t)((sk >> 11) & 0x3ff) << 10) | ((uint32_t)((sk >> 21) & 3) << 20) |
+         ((uint32_t)Wt << 22);
+}
+
+// TransformLineFitPoint (apriltag_gpu.cu:631-687) of one compact point word
+__device__ __forceinline__ Mom6 point_mom(uint32_t cw) {
+  const int dxy = (int)((cw >> 20) & 3);
+  const uint32_t ix2 = (cw & 0x3ff) * 2 + dx_of(dxy) + 1;
+  const uint32_t iy2 = ((cw >> 10) & 0x3ff) * 2 + dy_of(dxy) + 1;
+  const uint32_t Wt = cw >> 22;
+  Mom6 m;
+  m.Mx = Wt * ix2;
+  m.My = Wt * iy2;
+  m.W = Wt;
+  // (int64_t)(int32 W * ix2 * ix2): the product wraps as int32, then sign-extends
+  m.Mxx = (uint64_t)(int64_t)(int32_t)(Wt * ix2 * ix2);
+  m.Mxy = (uint64_t)(int64_t)(int32_t)(Wt * ix2 * iy2);
+  m.Myy = (uint64_t)(int64_t)(int32_t)(Wt * iy2 * iy2);
+  return m;
+}
+
+__device__ __forceinline__ Moments to_moments(const Mom6& s, int32_t N) {
+  Moments m;
+  m.Mx = (int32_t)s.Mx; m.My = (int32_t)s.My; m.W = (int32_t)s.W;
+  m.Mxx = (int64_t)s.Mxx; m.Myy = (int64_t)s.Myy; m.Mxy = (int64_t)s.Mxy;
+  m.N = N;
+  return m;
+}
+
+// FitLineError (line_fit_filter.cu:22-36) of one window, as ErrorCalculator
+// evaluates it (float result)
+__device__ __forceinline__ float window_err(const Mom6& s, int32_t N) {
+  const Moments m = to_moments(s, N);
+  const int64_t Wl = m.W;
+  const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
+  const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
+  const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
+  const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
+  const float eig = ((float)(Cxx + Cyy) - h) / (float)((double)(Wl * Wl) * 8.0);
+  return (float)m.N * eig;
+}
+
+// Per-team shared state of one blob.  After the theta sort `keys` is reused:
+// u32 compact point words in bytes [0, 4n) and f32 window errors in bytes
+// [4 CAP, 4 CAP + 4n).  The union holds, in turn, the bucket-sort counts, the
+// peak keys and the 90 segment fits of FitQuads.
 template <int CAP>
+constexpr int kPeakCap = (CAP / 4 * 4 > 3200 ? CAP / 4 * 4 : 3200) / 8;
+
+template <int NT, int CAP>
 struct BlobShared {
-  uint64_t keys[CAP];  // point sort keys, later peak keys
+  uint64_t keys[CAP];
+  union {
+    uint32_t bcnt[CAP / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
+    uint64_t peaks[kPeakCap<CAP>];
+    struct {
+      // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
+      // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0)
+      double err[kNMaxima][kNMaxima];
+      double mse[kNMaxima][kNMaxima];
+      double p[kNMaxima][kNMaxima][2];
+    } seg;
+  } u;
+  // inclusive prefix moments at the indices FitQuads reads: [k] = P[pi[k]],
+  // [10 + k] = P[pi[k] - 1], [20] = P[n - 1]
+  uint32_t tMx[21], tMy[21], tW[21];
+  uint64_t tMxx[21], tMyy[21], tMxy[21];
+  // exclusive prefix of each thread's chunk (teams of more than one wave)
+  uint32_t bMx[NT > 64 ? NT : 1], bMy[NT > 64 ? NT : 1], bW[NT > 64 ? NT : 1];
+  uint64_t bMxx[NT > 64 ? NT : 1], bMyy[NT > 64 ? NT : 1], bMxy[NT > 64 ? NT : 1];
+  Mom6 wsum[NT / 64];
+  int64_t red7[NT / 64][8];
   double red_f64[16];
-  int64_t red_i64[16];
   uint32_t red_u32[16];
-  int32_t red_i32[16];
   uint32_t red_idx[16];
   uint32_t item, nwork, npeaks;
   int32_t pi[16];
-  uint32_t bcnt[CAP / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
-  uint32_t bmax;
-  // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
-  // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0)
-  double seg_err[kNMaxima][kNMaxima];
-  double seg_mse[kNMaxima][kNMaxima];
-  double seg_p[kNMaxima][kNMaxima][2];
   double lines[4][4];
+  uint32_t pacc[21];  // probe accumulators + processed-point count of this team
+  uint64_t t_last;
 };
 
 // Sort of a blob's (theta, plane, y, x) keys: theta is near-uniform around the
@@ -1187,17 +1311,18 @@ struct BlobShared {
 constexpr uint64_t kThetaSpan = 50265600;  // > max theta = rint((2 pi) * 8e6)
 
 template <int NT, int CAP>
-__device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
+__device__ bool team_bucket_sort(BlobShared<NT, CAP>& S, int n) {
   if (n < 64 || 2 * n > CAP) return false;
   const int tid = team_rank<NT>();
   int nb = 32;
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= CAP/2
   auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> 23) * (uint64_t)nb) / kThetaSpan); };
-  for (int i = tid; i < nb / 2; i += NT) S.bcnt[i] = 0;
+  uint32_t* bcnt = S.u.bcnt;
+  for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
   team_sync<NT>();
   for (int t = tid; t < n; t += NT) {
     const uint32_t bk = bucket(S.keys[t]);
-    atomicAdd(&S.bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+    atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
   }
   team_sync<NT>();
   // exclusive scan of the nb counts: each thread owns nb/NT (or 1) consecutive buckets
@@ -1210,7 +1335,7 @@ __device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
     cval[j] = 0;
     if (j < per && b0 + j < nb) {
       const uint32_t bb = (uint32_t)(b0 + j);
-      cval[j] = (S.bcnt[bb >> 1] >> ((bb & 1) * 16)) & 0xffffu;
+      cval[j] = (bcnt[bb >> 1] >> ((bb & 1) * 16)) & 0xffffu;
       loc += cval[j];
       mx = cval[j] > mx ? cval[j] : mx;
     }
@@ -1228,7 +1353,7 @@ __device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
       const uint32_t bb = (uint32_t)(b0 + j);  // even: owns the whole word when per >= 2
       if (per >= 2) {
         const uint32_t s0 = run, s1 = run + cval[j];
-        S.bcnt[bb >> 1] = s0 | (s1 << 16);
+        bcnt[bb >> 1] = s0 | (s1 << 16);
       }
     }
     if (j < per && b0 + j < nb) run += cval[j];
@@ -1237,14 +1362,14 @@ __device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
     // one bucket per thread: neighbours share a word; even lane writes both halves
     const uint32_t mine = incl - loc;
     const uint32_t other = __shfl_down(mine, 1);
-    if ((b0 & 1) == 0) S.bcnt[b0 >> 1] = mine | (other << 16);
+    if ((b0 & 1) == 0) bcnt[b0 >> 1] = mine | (other << 16);
   }
   team_sync<NT>();
   uint64_t* T = S.keys + CAP / 2;
   for (int t = tid; t < n; t += NT) {
     const uint64_t k = S.keys[t];
     const uint32_t bk = bucket(k);
-    const uint32_t old = atomicAdd(&S.bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+    const uint32_t old = atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
     T[(old >> ((bk & 1) * 16)) & 0xffffu] = k;
   }
   team_sync<NT>();
@@ -1262,39 +1387,517 @@ __device__ bool team_bucket_sort(BlobShared<CAP>& S, int n) {
   return true;
 }
 
-// Processes one work item (frame, pair rank) with a team of NT threads.
+// bitonic sort of n (power of two) peak keys: slots below cap in LDS, the rest
+// in the team's global overflow area (kGlob: large blobs with pathological peak
+// counts only; the small-blob LDS area always holds n/2 peaks)
+template <bool kGlob>
+__device__ __forceinline__ uint64_t pk_get(const uint64_t* lds, const uint64_t* gpk, int cap, int i) {
+  if constexpr (kGlob) return i < cap ? lds[i] : gpk[i - cap];
+  else return lds[i];
+}
+template <bool kGlob>
+__device__ __forceinline__ void pk_put(uint64_t* lds, uint64_t* gpk, int cap, int i, uint64_t v) {
+  if constexpr (kGlob) {
+    if (i < cap) lds[i] = v;
+    else gpk[i - cap] = v;
+  } else {
+    lds[i] = v;
+  }
+}
+template <int NT, bool kGlob>
+__device__ void team_bitonic_sort_pk(uint64_t* lds, uint64_t* gpk, int cap, int n) {
+  const int r = team_rank<NT>();
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = r; i < n; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = pk_get<kGlob>(lds, gpk, cap, i), c = pk_get<kGlob>(lds, gpk, cap, ixj);
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) {
+            pk_put<kGlob>(lds, gpk, cap, i, c);
+            pk_put<kGlob>(lds, gpk, cap, ixj, a);
+          }
+        }
+      }
+      team_sync<NT>();
+    }
+  }
+}
+
+// one extents reduction of seven values across the team (P3 MinMaxExtents)
 template <int NT, int CAP>
-__device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<CAP>& S,
-                          const BlobScratch& Pg, const BlobScratch* Pl, uint32_t lcap, uint32_t w, uint32_t* pacc) {
+__device__ __forceinline__ void team_extents(BlobShared<NT, CAP>& S, uint32_t& mnx, uint32_t& mxx, uint32_t& mny,
+                                             uint32_t& mxy, int32_t& sgx, int32_t& sgy, int64_t& spg) {
+  mnx = wave_reduce(mnx, MinOp()); mxx = wave_reduce(mxx, MaxOp());
+  mny = wave_reduce(mny, MinOp()); mxy = wave_reduce(mxy, MaxOp());
+  sgx = wave_reduce(sgx, AddOp()); sgy = wave_reduce(sgy, AddOp());
+  spg = wave_reduce(spg, AddOp());
+  if constexpr (NT > 64) {
+    const int w = threadIdx.x >> 6;
+    team_sync<NT>();
+    if (lane_id() == 0) {
+      S.red7[w][0] = mnx; S.red7[w][1] = mxx; S.red7[w][2] = mny; S.red7[w][3] = mxy;
+      S.red7[w][4] = sgx; S.red7[w][5] = sgy; S.red7[w][6] = spg;
+    }
+    team_sync<NT>();
+    for (int i = 0; i < NT / 64; i++) {
+      mnx = min(mnx, (uint32_t)S.red7[i][0]); mxx = max(mxx, (uint32_t)S.red7[i][1]);
+      mny = min(mny, (uint32_t)S.red7[i][2]); mxy = max(mxy, (uint32_t)S.red7[i][3]);
+    }
+    int32_t gx = 0, gy = 0;
+    int64_t pg = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      gx += (int32_t)S.red7[i][4]; gy += (int32_t)S.red7[i][5]; pg += S.red7[i][6];
+    }
+    sgx = gx; sgy = gy; spg = pg;
+  }
+}
+
+// Exclusive team scan of each thread's chunk moments (one pass for all six);
+// *total = the sum over the team
+template <int NT, int CAP>
+__device__ __forceinline__ Mom6 team_excl_scan_mom(BlobShared<NT, CAP>& S, const Mom6& v, Mom6* total) {
+  const uint32_t lane = lane_id();
+  Mom6 incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const Mom6 u = mom_shfl_up(incl, d);
+    if (lane >= (uint32_t)d) mom_add(incl, u);
+  }
+  Mom6 ex = incl;
+  mom_sub(ex, v);
+  if constexpr (NT > 64) {
+    const int w = threadIdx.x >> 6;
+    team_sync<NT>();
+    if (lane == 63) S.wsum[w] = incl;
+    team_sync<NT>();
+    Mom6 tot = mom_zero();
+    for (int i = 0; i < NT / 64; i++) {
+      if (i < w) mom_add(ex, S.wsum[i]);
+      mom_add(tot, S.wsum[i]);
+    }
+    *total = tot;
+  } else {
+    *total = mom_shfl(incl, 63);
+  }
+  return ex;
+}
+
+// Inclusive prefix moments P(i) of the blob's points: the owning chunk's base
+// plus the chunk's words up to i.  Called by every lane of the team (the base
+// of a wave-sized team comes by lane shuffle); inactive lanes get zero.
+template <int NT, int CAP>
+__device__ __forceinline__ Mom6 prefix_at(const BlobShared<NT, CAP>& S, const uint32_t* cw, const Mom6& cbase,
+                                          uint32_t c, uint32_t i, bool active) {
+  const uint32_t o = active ? i / c : 0;
+  Mom6 p;
+  if constexpr (NT == 64) {
+    p = mom_shfl(cbase, (int)o);
+  } else {
+    p = Mom6{S.bMx[o], S.bMy[o], S.bW[o], S.bMxx[o], S.bMyy[o], S.bMxy[o]};
+  }
+  if (!active) return mom_zero();
+  for (uint32_t j = o * c; j <= i; j++) mom_add(p, point_mom(cw[j]));
+  return p;
+}
+
+// Processes one work item (frame, pair rank) with a team of NT threads.
+// gpk: this team's global overflow area for peak keys beyond kPeakCap (large
+// blobs only; nullptr when the LDS area always suffices).
+template <int NT, int CAP>
+__device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S, uint64_t* gpk,
+                          const uint32_t* combo, uint32_t w, uint32_t* pacc) {
+  constexpr int kC = (CAP + NT - 1) / NT;  // max points per thread chunk
+  constexpr int kPk = kPeakCap<CAP>;
+  constexpr bool kGlobPk = kPk < CAP / 2;  // peaks (<= n/2) may overflow the LDS area
+  static_assert(kC <= 32, "chunk too long");
   const int tid = team_rank<NT>();
   const uint32_t lane = lane_id();
-  // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k])
-  uint64_t t_last = prm.probe ? wall_clock64() : 0;
-  auto phase = [&](int k) {  // accumulated per team in registers, flushed once per kernel
+  // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k]);
+  // the accumulators live in the team's LDS, not in registers
+  if (prm.probe && tid == 0) S.t_last = wall_clock64();
+  auto phase = [&](int k) {  // accumulated per team, flushed once per kernel
     if (prm.probe && tid == 0) {
       const uint64_t now = wall_clock64();
-      pacc[k] += (uint32_t)(now - t_last);
+      pacc[k] += (uint32_t)(now - S.t_last);
       pacc[10 + k] += 1;
-      t_last = now;
+      S.t_last = now;
     }
   };
+  const int f = (int)(w >> 16);
+  const uint32_t rank = w & 0xffff;
+  const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+  if (tid == 0) pacc[20] += n;  // points this team processed (batch statistics)
+  const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
+  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
+  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+
+  // extents, SelectBlobs and the theta keys come from k_extents
+  if (b.pair_sel[(size_t)f * kMaxPairs + rank] == 0) return;  // uniform across the team
+  const uint32_t bi = rank & 0xfff;
+  phase(0);
+  for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
+  phase(1);
+  team_sync<NT>();
+  if (!team_bucket_sort<NT, CAP>(S, (int)n)) {
+    int np2 = 64;
+    while (np2 < (int)n) np2 <<= 1;
+    for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
+    team_sync<NT>();
+    team_bitonic_sort<uint64_t, NT>(S.keys, np2);
+  }
+  phase(2);
+  if (prm.diag_stop == 2) return;
+
+  // ---- line-fit points (P7): blocked chunks, W from the decimated gradient,
+  // sorted keys -> compact words in place; chunk sums -> exclusive team scan
+  const uint32_t c = (n + NT - 1) / NT;
+  const uint32_t t0 = min(n, (uint32_t)tid * c), t1 = min(n, t0 + c);
+  uint32_t* cw = reinterpret_cast<uint32_t*>(S.keys);
+  float* errv = reinterpret_cast<float*>(S.keys) + CAP;
+  uint32_t word[kC];
+  Mom6 csum = mom_zero();
+#pragma unroll
+  for (int k = 0; k < kC; k++) {
+    word[k] = 0;
+    if (k >= (int)c) break;  // c is uniform across the team
+    const uint32_t t = t0 + k;
+    if (t < t1) {
+      const uint64_t sk = S.keys[t];
+      const int dxy = (int)((sk >> 21) & 3);
+      const int32_t ix2 = (int32_t)(((sk >> 1) & 0x3ff) * 2 + dx_of(dxy)) + 1;
+      const int32_t iy2 = (int32_t)(((sk >> 11) & 0x3ff) * 2 + dy_of(dxy)) + 1;
+      const int32_t ix = ix2 / 2, iy = iy2 / 2;
+      int32_t Wt = 1;
+      if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
+        const int32_t gxv = (int32_t)dec[iy * g.Wd + ix + 1] - (int32_t)dec[iy * g.Wd + ix - 1];
+        const int32_t gyv = (int32_t)dec[(iy + 1) * g.Wd + ix] - (int32_t)dec[(iy - 1) * g.Wd + ix];
+        Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+      }
+      word[k] = compact_word(sk, Wt);
+      // parity tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
+      const uint64_t pbits = (((sk >> 1) & 0x3ff) << 14) | (((sk >> 11) & 0x3ff) << 4) | ((sk & 1) << 3) |
+                             ((sk >> 21) & 3);
+      if (prm.taps) grp[t] = ((uint64_t)bi << 52) | (((sk >> 23) & 0xfffffff) << 24) | pbits;
+      mom_add(csum, point_mom(word[k]));
+    }
+  }
+  team_sync<NT>();  // every key read before the compact words overwrite them
+#pragma unroll
+  for (int k = 0; k < kC; k++) {
+    if (k >= (int)c) break;
+    if (t0 + k < t1) cw[t0 + k] = word[k];
+  }
+  Mom6 total;
+  const Mom6 cbase = team_excl_scan_mom<NT, CAP>(S, csum, &total);
+  if constexpr (NT > 64) {
+    S.bMx[tid] = cbase.Mx; S.bMy[tid] = cbase.My; S.bW[tid] = cbase.W;
+    S.bMxx[tid] = cbase.Mxx; S.bMyy[tid] = cbase.Myy; S.bMxy[tid] = cbase.Mxy;
+  }
+  team_sync<NT>();
+  phase(3);
+  if (prm.diag_stop == 3) return;
+
+  // ---- errors (K10 ErrorCalculator, restated per blob, cyclic): the window
+  // [t0 - ksz, t0 + ksz] of the chunk's first point from two prefix lookups
+  // (P(hi) - P(lo - 1), plus the total when it wraps), then slid across the chunk
+  const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
+  const int32_t Nw = (int32_t)(2 * ksz + 1);
+  const bool act = t0 < t1;
+  {
+    const int lo = (int)t0 - (int)ksz, hi = (int)t0 + (int)ksz;
+    const int ia = hi >= (int)n ? hi - (int)n : hi;
+    const int ib = (lo >= 0 ? lo : lo + (int)n) - 1;
+    const Mom6 pa = prefix_at<NT, CAP>(S, cw, cbase, c, (uint32_t)ia, act);
+    const Mom6 pb = prefix_at<NT, CAP>(S, cw, cbase, c, (uint32_t)(ib >= 0 ? ib : 0), act && ib >= 0);
+    Mom6 s = pa;
+    mom_sub(s, pb);
+    if (lo < 0 || hi >= (int)n) mom_add(s, total);
+    if (act) errv[t0] = window_err(s, Nw);
+    for (uint32_t t = t0 + 1; t < t1; t++) {
+      uint32_t ja = t + ksz, jr = t + n - ksz - 1;
+      ja -= ja >= n ? n : 0;
+      jr -= jr >= n ? n : 0;
+      mom_add(s, point_mom(cw[ja]));
+      mom_sub(s, point_mom(cw[jr]));
+      errv[t] = window_err(s, Nw);
+    }
+  }
+  if (tid == 0) S.npeaks = 0;
+  team_sync<NT>();
+  phase(4);
+
+  // ---- 7-tap filter and strict local maxima; peak keys (P8-P10: -filtered
+  // error in cub's float radix order, then point index)
+  auto filt_at = [&](uint32_t t) -> double {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+      uint32_t idx = t + n + j - 3;
+      idx -= idx >= n ? n : 0;
+      idx -= idx >= n ? n : 0;
+      acc += (double)errv[idx] * (double)c_filter[j];
+    }
+    return acc;
+  };
+  uint64_t* pks = S.u.peaks;
+  if (t0 < t1) {
+    double fprev = filt_at(t0 == 0 ? n - 1 : t0 - 1), fcur = filt_at(t0);
+    for (uint32_t t = t0; t < t1; t++) {
+      const double fnext = filt_at(t + 1 == n ? 0 : t + 1);
+      if (fcur > fprev && fcur > fnext) {
+        const float ef = (float)(-fcur);
+        uint32_t u = __float_as_uint(ef);
+        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // cub radix float order
+        const uint32_t slot = atomicAdd(&S.npeaks, 1u);
+        pk_put<kGlobPk>(pks, gpk, kPk, (int)slot, ((uint64_t)u << 32) | t);
+      }
+      fprev = fcur;
+      fcur = fnext;
+    }
+  }
+  team_sync<NT>();
+  const uint32_t npk = S.npeaks;
+  {
+    int p2 = 2;
+    while (p2 < (int)npk) p2 <<= 1;
+    for (int t = (int)npk + tid; t < p2; t += NT) pk_put<kGlobPk>(pks, gpk, kPk, t, ~0ull);
+    team_sync<NT>();
+    if (npk > 1) team_bitonic_sort_pk<NT, kGlobPk>(pks, gpk, kPk, p2);
+  }
+  phase(5);
+  if (prm.diag_stop == 4) return;
+  // ---- FitQuads (K11) --------------------------------------------------------
+  const int cnt = (int)npk;
+  if (tid < 16) {
+    // top min(10, cnt) peaks, re-sorted by point index (WarpMergeSort), pad 0xffff
+    const int v = (tid < cnt && tid < kNMaxima) ? (int)(pks[tid] & 0xffffffffu) : 0xffff;
+    int r = 0;
+    for (int j = 0; j < 16; j++) {
+      const int u = (j < cnt && j < kNMaxima) ? (int)(pks[j] & 0xffffffffu) : 0xffff;
+      r += (u < v) || (u == v && j < tid);
+    }
+    S.pi[r] = v;
+  }
+  team_sync<NT>();
+  // inclusive prefix moments at pi[k], pi[k] - 1 and n - 1: the owning chunk's
+  // base plus the chunk's words up to the index
+  {
+    const int k = tid;
+    uint32_t idx = 0;
+    bool need = false;
+    if (k < 10) { need = k < cnt && k < kNMaxima; idx = need ? (uint32_t)S.pi[k] : 0; }
+    else if (k < 20) { need = k - 10 < cnt && k - 10 < kNMaxima && S.pi[k - 10] > 0; idx = need ? (uint32_t)S.pi[k - 10] - 1 : 0; }
+    else if (k == 20) { need = true; idx = n - 1; }
+    const Mom6 p = prefix_at<NT, CAP>(S, cw, cbase, c, idx, need);
+    if (need) {
+      S.tMx[k] = p.Mx; S.tMy[k] = p.My; S.tW[k] = p.W;
+      S.tMxx[k] = p.Mxx; S.tMyy[k] = p.Myy; S.tMxy[k] = p.Mxy;
+    }
+  }
+  team_sync<NT>();
+  phase(6);
+  // read_moments (line_fit_filter.cu:745-796) of the segment pi[a] -> pi[b]
+  auto seg_moments = [&](int a, int bb) -> Moments {
+    const uint32_t i0 = (uint32_t)S.pi[a], i1 = (uint32_t)S.pi[bb];
+    Mom6 m = Mom6{S.tMx[bb], S.tMy[bb], S.tW[bb], S.tMxx[bb], S.tMyy[bb], S.tMxy[bb]};
+    const Mom6 pm = Mom6{S.tMx[10 + a], S.tMy[10 + a], S.tW[10 + a], S.tMxx[10 + a], S.tMyy[10 + a], S.tMxy[10 + a]};
+    int32_t N;
+    if (i0 < i1) {
+      if (i0 > 0) mom_sub(m, pm);
+      N = (int32_t)(i1 - i0 + 1);
+    } else {
+      Mom6 z = Mom6{S.tMx[20], S.tMy[20], S.tW[20], S.tMxx[20], S.tMyy[20], S.tMxy[20]};
+      mom_sub(z, pm);
+      mom_add(z, m);
+      m = z;
+      N = (int32_t)(n - i0 + i1 + 1);
+    }
+    return to_moments(m, N);
+  };
+  // every segment a combination can use, fitted once (FitLine on the same
+  // moments as QuadFitCalculator's per-combination fits: identical results)
+  for (int ci = tid; cnt >= 4 && ci < kNMaxima * kNMaxima; ci += NT) {
+    const int a = ci / kNMaxima, bb = ci % kNMaxima;
+    if (a != bb && a < cnt && bb < cnt) {
+      const LineFitOut o = fit_line_v<false, true>(seg_moments(a, bb));
+      S.u.seg.err[a][bb] = o.err;
+      S.u.seg.mse[a][bb] = o.mse;
+      S.u.seg.p[a][bb][0] = o.p23[0];
+      S.u.seg.p[a][bb][1] = o.p23[1];
+    }
+  }
+  team_sync<NT>();
+  phase(7);
+  if (prm.diag_stop == 7) return;
+  // 210 lexicographic combinations; each lane keeps its first minimum
+  double err = DBL_MAX;
+  uint32_t bt = 0xffffffffu;
+  const double mse_max = (double)prm.max_line_fit_mse;
+  for (int ci = tid; ci < 210; ci += NT) {
+    double e4 = DBL_MAX;
+    if (cnt >= 4) {
+      const uint32_t cb = combo[ci];  // LDS copy of c_combo: no vector-memory wait in this loop
+      const int m0 = cb & 0xff, m1 = (cb >> 8) & 0xff, m2 = (cb >> 16) & 0xff, m3 = cb >> 24;
+      if (m3 < cnt && !(S.u.seg.mse[m0][m1] > mse_max)) {
+        if (!(S.u.seg.mse[m1][m2] > mse_max)) {
+          const double dot =
+              S.u.seg.p[m0][m1][0] * S.u.seg.p[m1][m2][0] + S.u.seg.p[m0][m1][1] * S.u.seg.p[m1][m2][1];
+          if (!(fabs(dot) > prm.cos_critical_rad)) {
+            if (!(S.u.seg.mse[m2][m3] > mse_max) && !(S.u.seg.mse[m3][m0] > mse_max))
+              e4 = S.u.seg.err[m0][m1] + S.u.seg.err[m1][m2] + S.u.seg.err[m2][m3] + S.u.seg.err[m3][m0];
+          }
+        }
+      }
+    }
+    if (bt == 0xffffffffu || e4 < err) { err = e4; bt = (uint32_t)ci; }
+  }
+  // BlockReduce(MinQuadError): minimum error, first (lowest) combination on ties
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const double oe = __shfl_xor(err, d);
+    const uint32_t ot = __shfl_xor(bt, d);
+    if (oe < err || (oe == err && ot < bt)) { err = oe; bt = ot; }
+  }
+  if constexpr (NT > 64) {
+    if (lane == 0) { S.red_f64[tid >> 6] = err; S.red_idx[tid >> 6] = bt; }
+    team_sync<NT>();
+    err = S.red_f64[0];
+    bt = S.red_idx[0];
+    for (int i = 1; i < NT / 64; i++)
+      if (S.red_f64[i] < err || (S.red_f64[i] == err && S.red_idx[i] < bt)) { err = S.red_f64[i]; bt = S.red_idx[i]; }
+  }
+  phase(8);
+  if (prm.diag_stop == 8) return;
+  const double best = err;
+  if (bt >= 210) bt = 0;
+  const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
+  uint16_t qidx[4];
+  const uint32_t cbt = combo[bt];
+  for (int k = 0; k < 4; k++) qidx[k] = (uint16_t)S.pi[(cbt >> (8 * k)) & 0xff];
+  // UpdateFitQuads (apriltag_detect.cu:98-241): side lines in parallel, rest on one lane
+  if (valid && tid < 4) {
+    const LineFitOut o =
+        fit_line_v<true, true>(seg_moments((cbt >> (8 * tid)) & 0xff, (cbt >> (8 * ((tid + 1) & 3))) & 0xff));
+    S.lines[tid][0] = o.p01[0];
+    S.lines[tid][1] = o.p01[1];
+    S.lines[tid][2] = o.p23[0];
+    S.lines[tid][3] = o.p23[1];
+  }
+  team_sync<NT>();
+  if (tid == 0) {
+    QuadRecord rec;
+    rec.blob_index = bi;
+    rec.valid = valid;
+    for (int k = 0; k < 4; k++) rec.indices[k] = qidx[k];
+    float qc[4][2];
+    int ok = valid;
+    for (int k = 0; ok && k < 4; k++) {
+      const int k1 = (k + 1) & 3;
+      const double A00 = S.lines[k][3], A01 = -S.lines[k1][3];
+      const double A10 = -S.lines[k][2], A11 = S.lines[k1][2];
+      const double B0 = -S.lines[k][0] + S.lines[k1][0];
+      const double B1 = -S.lines[k][1] + S.lines[k1][1];
+      const double det = A00 * A11 - A10 * A01;
+      const double W00 = A11 / det, W01 = -A01 / det;
+      if (fabs(det) < 0.001) { ok = 0; break; }
+      const double L0 = W00 * B0 + W01 * B1;
+      qc[k][0] = (float)(S.lines[k][0] + L0 * A00);
+      qc[k][1] = (float)(S.lines[k][1] + L0 * A10);
+    }
+    if (ok) {
+      float area = 0, len[3], pp;
+      for (int k = 0; k < 3; k++) {
+        const int a2 = k, b2 = (k + 1) % 3;
+        len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+      }
+      pp = (len[0] + len[1] + len[2]) / 2;
+      area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+      const int idxs[4] = {2, 3, 0, 2};
+      for (int k = 0; k < 3; k++) {
+        const int a2 = idxs[k], b2 = idxs[k + 1];
+        len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+      }
+      pp = (len[0] + len[1] + len[2]) / 2;
+      area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+      if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
+    }
+    for (int k = 0; ok && k < 4; k++) {
+      const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
+      const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
+      const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
+      const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
+      if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) ok = 0;
+    }
+    QuadCand qcand;
+    for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
+      const float x = ok ? (qc[k][0] - 0.5f) * 2.0f + 0.5f : 0.f;
+      const float y = ok ? (qc[k][1] - 0.5f) * 2.0f + 0.5f : 0.f;
+      rec.corners[k][0] = qcand.p[k][0] = x;
+      rec.corners[k][1] = qcand.p[k][1] = y;
+    }
+    rec.accepted = ok;
+    b.quads[(size_t)f * kMaxPairs + rank] = rec;  // slot = pair rank: no returning atomic
+    atomicAdd(b.nquads + f, 1u);                  // count only (result unused: fire and forget)
+    if (ok && prm.diag_stop != 5) {
+      qcand.frame = (uint32_t)f;
+      qcand.rank = rank;
+      const uint32_t ci = atomicAdd(b.nqcand + f, 1u);  // per-frame counters spread the contention
+      if (ci < (uint32_t)kQuadCandPerFrame) b.qcand[(size_t)f * kQuadCandPerFrame + ci] = qcand;
+      else atomicOr(b.status + f, kStatusQuadsOverflow);
+    }
+  }
+  phase(9);
+  team_sync<NT>();
+}
+
+__device__ __forceinline__ void load_combos(uint32_t* s_combo, int tid, int nt) {
+  for (int i = tid; i < 210; i += nt)
+    s_combo[i] = (uint32_t)c_combo[i][0] | ((uint32_t)c_combo[i][1] << 8) | ((uint32_t)c_combo[i][2] << 16) |
+                 ((uint32_t)c_combo[i][3] << 24);
+}
+
+// ---------------------------------------------------------------------------
+// K8b: per candidate pair (one wave each, every size class): MinMaxExtents
+// (P3, line_fit_filter.h:14-59), SelectBlobs (apriltag_gpu.cu:534-559; tag36h11:
+// normal border only) and, for kept blobs, the (theta, plane, y, x) sort keys of
+// P5/P6 (apriltag_gpu.cu:380-412) written over the grouped points in place.
+// The blob kernels then see kept blobs only.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool work_item(const DevBufs& b, const uint32_t* cnt, int c0, int c1, uint32_t it,
+                                          uint32_t* w) {
+  for (int c = c0; c < c1; c++) {
+    if (it < cnt[c]) {
+      *w = b.work[(size_t)c * b.wcap + it];
+      return true;
+    }
+    it -= cnt[c];
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_extents(DevBufs b, Geom g) {
+  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const uint32_t lane = lane_id();
+  uint32_t cnt[kNumCls], total = 0;
+#pragma unroll
+  for (int c = 0; c < kNumCls; c++) {
+    cnt[c] = min(b.ncls[c], b.wcap);
+    total += cnt[c];
+  }
+  for (uint32_t it = gw; it < total; it += nw) {
+    uint32_t w = 0;
+    work_item(b, cnt, 0, kNumCls, it, &w);
     const int f = (int)(w >> 16);
     const uint32_t rank = w & 0xffff;
     const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
-    if (tid == 0) pacc[20] += n;  // points this team processed (batch statistics)
-    // prefix moments / errors in LDS when they fit the team's LDS scratch
-    const BlobScratch& P = (Pl && n <= lcap) ? *Pl : Pg;
-    const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
-    uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
-    const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
-
-    // ---- extents (P3) ---------------------------------------------------------
+    uint64_t* grp = b.grp + (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
     uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
     int32_t sgx = 0, sgy = 0;
     int64_t spg = 0;
-    for (uint32_t t = tid; t < n; t += NT) {
+    for (uint32_t t = lane; t < n; t += 64) {
       const uint64_t k = grp[t];
-      S.keys[t] = k;
       const int dxy = (int)(k & 3);
       const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
       const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
@@ -1305,28 +1908,18 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       spg += (int64_t)px * gx + (int64_t)py * gy;
     }
     Ext e;
-    e.min_x = team_reduce<NT>(mnx, MinOp(), S.red_u32);
-    e.max_x = team_reduce<NT>(mxx, MaxOp(), S.red_u32);
-    e.min_y = team_reduce<NT>(mny, MinOp(), S.red_u32);
-    e.max_y = team_reduce<NT>(mxy, MaxOp(), S.red_u32);
-    e.gx_sum = team_reduce<NT>(sgx, AddOp(), S.red_i32);
-    e.gy_sum = team_reduce<NT>(sgy, AddOp(), S.red_i32);
-    e.pg_sum = team_reduce<NT>(spg, AddOp(), S.red_i64);
+    e.min_x = wave_reduce(mnx, MinOp()); e.max_x = wave_reduce(mxx, MaxOp());
+    e.min_y = wave_reduce(mny, MinOp()); e.max_y = wave_reduce(mxy, MaxOp());
+    e.gx_sum = wave_reduce(sgx, AddOp()); e.gy_sum = wave_reduce(sgy, AddOp());
+    e.pg_sum = wave_reduce(spg, AddOp());
     e.count = n;
-    // ---- SelectBlobs (apriltag_gpu.cu:534-559); tag36h11: normal border only
     bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
     keep = keep && !((double)ext_dot(e) < 0.0);
-    phase(0);
-    if (!keep) return;  // uniform across the workgroup
-    phase(1);
-    if (prm.diag_stop == 1) return;
-    if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
-    const uint32_t bi = rank & 0xfff;
-
-    // ---- theta + sort key (P5/P6): (theta, plane, y, x) -----------------------
+    if (!keep) continue;  // uniform across the wave
+    if (lane == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
     const double cx = ext_cx(e), cy = ext_cy(e);
-    for (uint32_t t = tid; t < n; t += NT) {
-      const uint64_t k = S.keys[t];
+    for (uint32_t t = lane; t < n; t += 64) {
+      const uint64_t k = grp[t];
       const int dxy = (int)(k & 3);
       const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
       const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
@@ -1336,274 +1929,12 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       long long ti = (long long)rintf(theta);
       if (ti < 0) ti = 0;
       // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
-      S.keys[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
-                  ((uint64_t)bx << 1) | ((k >> 3) & 1);
+      grp[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
+               ((uint64_t)bx << 1) | ((k >> 3) & 1);
     }
-    team_sync<NT>();
-    if (!team_bucket_sort<NT, CAP>(S, (int)n)) {
-      int np2 = 64;
-      while (np2 < (int)n) np2 <<= 1;
-      for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
-      team_sync<NT>();
-      team_bitonic_sort<uint64_t, NT>(S.keys, np2);
-    }
-    phase(2);
-    if (prm.diag_stop == 2) return;
-
-    // ---- line-fit points + per-blob inclusive prefix sums (P7) -----------------
-    {
-      // Mx, My, W are int32 in the reference (LineFitPoint): wrap like two's complement
-      uint32_t cMx = 0, cMy = 0, cW = 0;
-      int64_t cMxx = 0, cMyy = 0, cMxy = 0;
-      for (uint32_t base = 0; base < n; base += NT) {
-        const uint32_t t = base + tid;
-        uint32_t vMx = 0, vMy = 0, vW = 0;
-        int64_t vMxx = 0, vMyy = 0, vMxy = 0;
-        if (t < n) {
-          const uint64_t sk = S.keys[t];
-          const int dxy = (int)((sk >> 21) & 3);
-          const int32_t ix2 = (int32_t)(((sk >> 1) & 0x3ff) * 2 + dx_of(dxy)) + 1;
-          const int32_t iy2 = (int32_t)(((sk >> 11) & 0x3ff) * 2 + dy_of(dxy)) + 1;
-          const int32_t ix = ix2 / 2, iy = iy2 / 2;
-          int32_t Wt = 1;
-          if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
-            const int32_t gxv = (int32_t)dec[(size_t)iy * g.Wd + ix + 1] - (int32_t)dec[(size_t)iy * g.Wd + ix - 1];
-            const int32_t gyv = (int32_t)dec[(size_t)(iy + 1) * g.Wd + ix] - (int32_t)dec[(size_t)(iy - 1) * g.Wd + ix];
-            Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
-          }
-          vMx = (uint32_t)(Wt * ix2); vMy = (uint32_t)(Wt * iy2); vW = (uint32_t)Wt;
-          vMxx = (int64_t)(Wt * ix2 * ix2); vMxy = (int64_t)(Wt * ix2 * iy2); vMyy = (int64_t)(Wt * iy2 * iy2);
-        }
-        uint32_t tot;
-        int64_t tot64;
-        const uint32_t pMx = team_incl_scan<NT>(vMx, S.red_u32, &tot) + cMx; cMx += tot;
-        const uint32_t pMy = team_incl_scan<NT>(vMy, S.red_u32, &tot) + cMy; cMy += tot;
-        const uint32_t pW = team_incl_scan<NT>(vW, S.red_u32, &tot) + cW; cW += tot;
-        const int64_t pMxx = team_incl_scan<NT>(vMxx, S.red_i64, &tot64) + cMxx; cMxx += tot64;
-        const int64_t pMyy = team_incl_scan<NT>(vMyy, S.red_i64, &tot64) + cMyy; cMyy += tot64;
-        const int64_t pMxy = team_incl_scan<NT>(vMxy, S.red_i64, &tot64) + cMxy; cMxy += tot64;
-        if (t < n) {
-          P.Mx[t] = (int32_t)pMx; P.My[t] = (int32_t)pMy; P.W[t] = (int32_t)pW;
-          P.Mxx[t] = pMxx; P.Myy[t] = pMyy; P.Mxy[t] = pMxy;
-          // parity tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
-          const uint64_t sk = S.keys[t];
-          const uint64_t pbits = (((sk >> 1) & 0x3ff) << 14) | (((sk >> 11) & 0x3ff) << 4) | ((sk & 1) << 3) |
-                                 ((sk >> 21) & 3);
-          grp[t] = ((uint64_t)bi << 52) | (((sk >> 23) & 0xfffffff) << 24) | pbits;
-        }
-      }
-    }
-    team_sync<NT>();
-    phase(3);
-    if (prm.diag_stop == 3) return;
-    // ---- errors, filter, peaks (K10 restated per blob, cyclic) ----------------
-    const uint32_t ksz = n / 12 < 20 ? n / 12 : 20;
-    for (uint32_t t = tid; t < n; t += NT) {
-      const uint32_t i0 = (t + 2 * n - ksz) % n, i1 = (t + n + ksz) % n;
-      const Moments m = read_moments(P, n, i0, i1);
-      const int64_t Wl = m.W;
-      const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
-      const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
-      const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
-      const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
-      const float eig = ((float)(Cxx + Cyy) - h) / (float)((double)(Wl * Wl) * 8.0);
-      P.err[t] = (double)((float)m.N * eig);
-    }
-    team_sync<NT>();
-    for (uint32_t t = tid; t < n; t += NT) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < 7; j++) {
-        const uint32_t idx = (uint32_t)((int64_t)t + j - 3 + n) % n;
-        acc += P.err[idx] * (double)c_filter[j];
-      }
-      P.filt[t] = acc;
-    }
-    if (tid == 0) S.npeaks = 0;
-    team_sync<NT>();
-    for (uint32_t t = tid; t < n; t += NT) {
-      const double me = P.filt[t];
-      const double bef = P.filt[(t + n - 1) % n], aft = P.filt[(t + 1) % n];
-      if (me > bef && me > aft) {
-        const float ef = (float)(-me);
-        uint32_t u = __float_as_uint(ef);
-        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // cub radix float order
-        const uint32_t slot = atomicAdd(&S.npeaks, 1u);
-        S.keys[slot] = ((uint64_t)u << 32) | t;
-      }
-    }
-    team_sync<NT>();
-    const uint32_t npk = S.npeaks;
-    {
-      int p2 = 2;
-      while (p2 < (int)npk) p2 <<= 1;
-      for (int t = (int)npk + tid; t < p2; t += NT) S.keys[t] = ~0ull;
-      team_sync<NT>();
-      if (npk > 1) team_bitonic_sort<uint64_t, NT>(S.keys, p2);
-    }
-    phase(4);
-    if (prm.diag_stop == 4) return;
-    // ---- FitQuads (K11) --------------------------------------------------------
-    const int cnt = (int)npk;
-    if (tid < 16) {
-      // top min(10, cnt) peaks, re-sorted by point index (WarpMergeSort), pad 0xffff
-      const int v = (tid < cnt && tid < kNMaxima) ? (int)(S.keys[tid] & 0xffffffffu) : 0xffff;
-      int r = 0;
-      for (int j = 0; j < 16; j++) {
-        const int u = (j < cnt && j < kNMaxima) ? (int)(S.keys[j] & 0xffffffffu) : 0xffff;
-        r += (u < v) || (u == v && j < tid);
-      }
-      S.pi[r] = v;
-    }
-    team_sync<NT>();
-    // every segment a combination can use, fitted once (FitLine on the same
-    // moments as QuadFitCalculator's per-combination fits: identical results)
-    for (int c = tid; cnt >= 4 && c < kNMaxima * kNMaxima; c += NT) {
-      const int a = c / kNMaxima, bb = c % kNMaxima;
-      if (a != bb && a < cnt && bb < cnt) {
-        const LineFitOut o = fit_line_v<false, true>(read_moments(P, n, S.pi[a], S.pi[bb]));
-        S.seg_err[a][bb] = o.err;
-        S.seg_mse[a][bb] = o.mse;
-        S.seg_p[a][bb][0] = o.p23[0];
-        S.seg_p[a][bb][1] = o.p23[1];
-      }
-    }
-    team_sync<NT>();
-    phase(7);
-    if (prm.diag_stop == 7) return;
-    // 210 lexicographic combinations; each lane keeps its first minimum
-    double err = DBL_MAX;
-    uint32_t bt = 0xffffffffu;
-    const double mse_max = (double)prm.max_line_fit_mse;
-    for (int c = tid; c < 210; c += NT) {
-      double e4 = DBL_MAX;
-      if (cnt >= 4) {
-        const int m0 = c_combo[c][0], m1 = c_combo[c][1], m2 = c_combo[c][2], m3 = c_combo[c][3];
-        if (m3 < cnt && !(S.seg_mse[m0][m1] > mse_max)) {
-          if (!(S.seg_mse[m1][m2] > mse_max)) {
-            const double dot = S.seg_p[m0][m1][0] * S.seg_p[m1][m2][0] + S.seg_p[m0][m1][1] * S.seg_p[m1][m2][1];
-            if (!(fabs(dot) > prm.cos_critical_rad)) {
-              if (!(S.seg_mse[m2][m3] > mse_max) && !(S.seg_mse[m3][m0] > mse_max))
-                e4 = S.seg_err[m0][m1] + S.seg_err[m1][m2] + S.seg_err[m2][m3] + S.seg_err[m3][m0];
-            }
-          }
-        }
-      }
-      if (bt == 0xffffffffu || e4 < err) { err = e4; bt = (uint32_t)c; }
-    }
-    // BlockReduce(MinQuadError): minimum error, first (lowest) combination on ties
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-      const double oe = __shfl_xor(err, d);
-      const uint32_t ot = __shfl_xor(bt, d);
-      if (oe < err || (oe == err && ot < bt)) { err = oe; bt = ot; }
-    }
-    if constexpr (NT > 64) {
-      if (lane == 0) { S.red_f64[tid >> 6] = err; S.red_idx[tid >> 6] = bt; }
-      team_sync<NT>();
-      err = S.red_f64[0];
-      bt = S.red_idx[0];
-      for (int i = 1; i < NT / 64; i++)
-        if (S.red_f64[i] < err || (S.red_f64[i] == err && S.red_idx[i] < bt)) { err = S.red_f64[i]; bt = S.red_idx[i]; }
-    }
-    phase(8);
-    if (prm.diag_stop == 8) return;
-    double best = err;
-    if (bt >= 210) bt = 0;
-    const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
-    uint16_t qidx[4];
-    for (int k = 0; k < 4; k++) qidx[k] = (uint16_t)S.pi[c_combo[bt][k]];
-    // UpdateFitQuads (apriltag_detect.cu:98-241): side lines in parallel, rest on one lane
-    if (valid && tid < 4) {
-      const LineFitOut o = fit_line_v<true, true>(read_moments(P, n, qidx[tid], qidx[(tid + 1) & 3]));
-      S.lines[tid][0] = o.p01[0];
-      S.lines[tid][1] = o.p01[1];
-      S.lines[tid][2] = o.p23[0];
-      S.lines[tid][3] = o.p23[1];
-    }
-    team_sync<NT>();
-    if (tid == 0) {
-      QuadRecord rec;
-      rec.blob_index = bi;
-      rec.valid = valid;
-      for (int k = 0; k < 4; k++) rec.indices[k] = qidx[k];
-      float qc[4][2];
-      int ok = valid;
-      for (int k = 0; ok && k < 4; k++) {
-        const int k1 = (k + 1) & 3;
-        const double A00 = S.lines[k][3], A01 = -S.lines[k1][3];
-        const double A10 = -S.lines[k][2], A11 = S.lines[k1][2];
-        const double B0 = -S.lines[k][0] + S.lines[k1][0];
-        const double B1 = -S.lines[k][1] + S.lines[k1][1];
-        const double det = A00 * A11 - A10 * A01;
-        const double W00 = A11 / det, W01 = -A01 / det;
-        if (fabs(det) < 0.001) { ok = 0; break; }
-        const double L0 = W00 * B0 + W01 * B1;
-        qc[k][0] = (float)(S.lines[k][0] + L0 * A00);
-        qc[k][1] = (float)(S.lines[k][1] + L0 * A10);
-      }
-      if (ok) {
-        float area = 0, len[3], pp;
-        for (int k = 0; k < 3; k++) {
-          const int a2 = k, b2 = (k + 1) % 3;
-          len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
-        }
-        pp = (len[0] + len[1] + len[2]) / 2;
-        area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
-        const int idxs[4] = {2, 3, 0, 2};
-        for (int k = 0; k < 3; k++) {
-          const int a2 = idxs[k], b2 = idxs[k + 1];
-          len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
-        }
-        pp = (len[0] + len[1] + len[2]) / 2;
-        area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
-        if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
-      }
-      for (int k = 0; ok && k < 4; k++) {
-        const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
-        const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
-        const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
-        const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
-        if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) ok = 0;
-      }
-      QuadCand qcand;
-      for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
-        const float x = ok ? (qc[k][0] - 0.5f) * 2.0f + 0.5f : 0.f;
-        const float y = ok ? (qc[k][1] - 0.5f) * 2.0f + 0.5f : 0.f;
-        rec.corners[k][0] = qcand.p[k][0] = x;
-        rec.corners[k][1] = qcand.p[k][1] = y;
-      }
-      rec.accepted = ok;
-      const uint32_t qi = atomicAdd(b.nquads + f, 1u);
-      if (qi < (uint32_t)kMaxQuads) b.quads[(size_t)f * kMaxQuads + qi] = rec;
-      if (ok && prm.diag_stop != 5) {
-        qcand.frame = (uint32_t)f;
-        qcand.rank = rank;
-        const uint32_t ci = atomicAdd(b.nqcand, 1u);
-        if (ci < b.qcand_cap) b.qcand[ci] = qcand;
-        else atomicOr(b.status + f, kStatusQuadsOverflow);
-      }
-    }
-  phase(9);
-  team_sync<NT>();
+  }
 }
 
-__device__ __forceinline__ BlobScratch blob_scratch(int32_t* s_i32, int64_t* s_i64, double* s_f64, size_t team,
-                                                    int cap) {
-  BlobScratch P;
-  P.Mx = s_i32 + (team * 3 + 0) * cap;
-  P.My = s_i32 + (team * 3 + 1) * cap;
-  P.W = s_i32 + (team * 3 + 2) * cap;
-  P.Mxx = s_i64 + (team * 3 + 0) * cap;
-  P.Myy = s_i64 + (team * 3 + 1) * cap;
-  P.Mxy = s_i64 + (team * 3 + 2) * cap;
-  P.err = s_f64 + (team * 2 + 0) * cap;
-  P.filt = s_f64 + (team * 2 + 1) * cap;
-  return P;
-}
-
-// K9a (large blobs, > kSmallBlob points): one blob per 256-thread workgroup
-// iteration, persistent over the large work list.
 __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm, const uint32_t* pacc, int base,
                                             bool leader) {
   if (!prm.probe || !leader) return;
@@ -1613,55 +1944,63 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
   }
 }
 
-template <int NT>
+// K9a (large blobs, > kSmallBlob points): one blob per NT-thread workgroup
+// iteration, persistent over the large work list.
+template <int NT, int CAP>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
-  uint32_t pacc[21] = {0};
-  __shared__ BlobShared<kSortCap> S;
+  __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
-  const BlobScratch P = blob_scratch(b.s_i32, b.s_i64, b.s_f64, blockIdx.x, kSortCap);
-  if (tid == 0) S.nwork = *b.nwork;
+  uint32_t* pacc = S.pacc;
+  if (tid < 21) pacc[tid] = 0;
+  uint64_t* gpk = b.s_pk + (size_t)blockIdx.x * (kSortCap / 2);
+  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  load_combos(s_combo, tid, NT);
+  if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
   __syncthreads();
-  const uint32_t nwork = S.nwork;
+  uint32_t nwork = 0;
+  for (int c = 0; c < kNumLargeCls; c++) nwork += s_cnt[c];
+  // dynamic dequeue over the size-ordered list (longest first): large blobs
+  // vary 8x in cost, and there are few of them, so one atomic per item is cheap
   while (true) {
     if (tid == 0) S.item = atomicAdd(b.workhead, 1u);
     __syncthreads();
     const uint32_t item = S.item;
     __syncthreads();
     if (item >= nwork) break;
-    blob_item<NT, kSortCap>(b, g, prm, S, P, nullptr, 0, b.work[item], pacc);
+    uint32_t w = 0;
+    work_item(b, s_cnt, 0, kNumLargeCls, item, &w);
+    blob_item<NT, CAP>(b, g, prm, S, gpk, s_combo, w, pacc);
   }
+  __syncthreads();
   probe_flush(b, prm, pacc, 80, tid == 0);
   if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
-// waves per workgroup, persistent over the small work list.
-__global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params prm) {
-  uint32_t pacc[21] = {0};
-  __shared__ BlobShared<kSmallBlob> Ss[4];
+// waves per workgroup, persistent over the small work list.  Everything a blob
+// needs lives in its wave's LDS slice (no global scratch).
+static_assert(kPeakCap<kSmallBlob> >= kSmallBlob / 2, "small-blob peaks must fit in LDS");
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_blob_small(DevBufs b, Geom g, Params prm) {
+  __shared__ BlobShared<64, kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  BlobShared<kSmallBlob>& S = Ss[wave];
-  const BlobScratch P = blob_scratch(b.ss_i32, b.ss_i64, b.ss_f64, (size_t)blockIdx.x * 4 + wave, kSmallBlob);
-#if AT_LDS_BLOB
-  __shared__ int32_t l_i32[4][3][kLdsBlob];
-  __shared__ int64_t l_i64[4][3][kLdsBlob];
-  __shared__ double l_f64[4][2][kLdsBlob];
-  BlobScratch L;
-  L.Mx = l_i32[wave][0]; L.My = l_i32[wave][1]; L.W = l_i32[wave][2];
-  L.Mxx = l_i64[wave][0]; L.Myy = l_i64[wave][1]; L.Mxy = l_i64[wave][2];
-  L.err = l_f64[wave][0]; L.filt = l_f64[wave][1];
-  const BlobScratch* PL = &L;
-#else
-  const BlobScratch* PL = nullptr;
-#endif
-  const uint32_t nwork = *b.nwork_small;
-  while (true) {
-    uint32_t item = 0;
-    if (lane == 0) item = atomicAdd(b.workhead_small, 1u);
-    item = __shfl(item, 0);
-    if (item >= nwork) break;
-    blob_item<64, kSmallBlob>(b, g, prm, S, P, PL, kLdsBlob, b.work_small[item], pacc);
+  BlobShared<64, kSmallBlob>& S = Ss[wave];
+  uint32_t* pacc = S.pacc;
+  if (lane < 21) pacc[lane] = 0;
+  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  load_combos(s_combo, threadIdx.x, 256);
+  if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
+  __syncthreads();
+  uint32_t nwork = 0;
+  for (int c = kNumLargeCls; c < kNumCls; c++) nwork += s_cnt[c];
+  // static round-robin over the size-ordered list: no dequeue atomic (a
+  // device-scope atomic on one hot address is serviced at the memory side; one
+  // per small blob serialized every wave of the chip behind that address)
+  const uint32_t nwaves = gridDim.x * 4;
+  for (uint32_t item = blockIdx.x * 4 + wave; item < nwork; item += nwaves) {
+    uint32_t w = 0;
+    work_item(b, s_cnt, kNumLargeCls, kNumCls, item, &w);
+    blob_item<64, kSmallBlob>(b, g, prm, S, nullptr, s_combo, w, pacc);
   }
   probe_flush(b, prm, pacc, 64, lane == 0);
   if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
@@ -1675,6 +2014,13 @@ __global__ __launch_bounds__(256) void k_blob_small(DevBufs b, Geom g, Params pr
 // decision scores) run on one lane in the reference's order.
 // ---------------------------------------------------------------------------
 constexpr int kDecodeThreads = 64;
+// quad_decode border patterns (x0, y0, dx, dy, is_white) for width_at_border 8
+__constant__ float c_border_pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0, 1, 0}, {8.5f, .5f, 0, 1, 1},
+                                         {7.5f, .5f, 0, 1, 0},   {0.5f, -0.5f, 1, 0, 1}, {0.5f, 0.5f, 1, 0, 0},
+                                         {0.5f, 8.5f, 1, 0, 1},  {0.5f, 7.5f, 1, 0, 0}};
+// cos / sin of rot * pi/2 as libm returns them (quad_decode's rotation of H)
+__constant__ double c_rot_c[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
+__constant__ double c_rot_s[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
 constexpr int kMaxRefineSamples = 1536;
 
 struct DecodeShared {
@@ -1684,6 +2030,7 @@ struct DecodeShared {
   float enx[4], eny[4];
   double lines[4][4];
   double H[9];
+  double A[72];  // homography DLT system
   double gmx[64], gmy[64], gmv[64];
   int gmvalid[64];
   double wC[3], bC[3];
@@ -1692,23 +2039,51 @@ struct DecodeShared {
   double margin;
   int ok;
   uint32_t item;
+  uint32_t qpre[kMaxBatch + 1];
 };
 
-__global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm) {
+__global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm, int B) {
   __shared__ DecodeShared S;
   const int tid = threadIdx.x;
-  while (true) {
-    if (tid == 0) S.item = atomicAdd(b.qhead, 1u);
-    __syncthreads();
-    const uint32_t item = S.item;
-    const uint32_t nq = min(*b.nqcand, b.qcand_cap);
-    __syncthreads();
-    if (item >= nq) break;
-    const QuadCand qd = b.qcand[item];
+  // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
+  uint32_t* qpre = S.qpre;
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int f = 0; f < B; f++) {
+      qpre[f] = acc;
+      acc += min(b.nqcand[f], (uint32_t)kQuadCandPerFrame);
+    }
+    qpre[B] = acc;
+  }
+  __syncthreads();
+  const uint32_t nq = qpre[B];
+  // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[128 + k], counts [160 + k])
+  uint32_t pacc[21] = {0};
+  uint64_t t_last = 0;
+  auto phase = [&](int k) {
+    if (prm.probe && tid == 0) {
+      const uint64_t now = wall_clock64();
+      if (k > 0) {
+        pacc[k] += (uint32_t)(now - t_last);
+        pacc[10 + k] += 1;
+      }
+      t_last = now;
+    }
+  };
+  for (uint32_t item = blockIdx.x; item < nq; item += gridDim.x) {  // static round-robin
+    int lo = 0, hi = B - 1;  // last frame whose prefix <= item
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (qpre[mid] <= item) lo = mid;
+      else hi = mid - 1;
+    }
+    const QuadCand& qd = b.qcand[(size_t)lo * kQuadCandPerFrame + (item - qpre[lo])];
     const int f = (int)qd.frame;
+    const uint32_t qrank = qd.rank;
     const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
     if (tid < 4) { S.qc[tid][0] = qd.p[tid][0]; S.qc[tid][1] = qd.p[tid][1]; }
     __syncthreads();
+    phase(0);
     if (prm.refine_edges) {
       if (tid < 4) {
         const int a2 = tid, b2 = (tid + 1) & 3;
@@ -1739,16 +2114,31 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         const double alpha = (1.0 + s) / (nsamples + 1);
         const double x0 = alpha * S.qc[a2][0] + (1 - alpha) * S.qc[b2][0];
         const double y0 = alpha * S.qc[a2][1] + (1 - alpha) * S.qc[b2][1];
-        double Mn = 0, Mcount = 0;
-        for (double nn = -3.0; nn <= 3.0; nn += 0.25) {
+        // the 25 steps n = -3, -2.75, ..., 3 (exact in double): every gray load is
+        // issued before the first is consumed, then the sums run in step order
+        constexpr int kSteps = 25;
+        int g1v[kSteps], g2v[kSteps];
+#pragma unroll
+        for (int k = 0; k < kSteps; k++) {
+          const double nn = -3.0 + 0.25 * k;
           const int x1 = (int)(x0 + (nn + 1) * nx);
           const int y1 = (int)(y0 + (nn + 1) * ny);
-          if (x1 < 0 || x1 >= g.W || y1 < 0 || y1 >= g.H) continue;
           const int x2 = (int)(x0 + (nn - 1) * nx);
           const int y2 = (int)(y0 + (nn - 1) * ny);
-          if (x2 < 0 || x2 >= g.W || y2 < 0 || y2 >= g.H) continue;
-          const int g1 = gray[(size_t)y1 * g.W + x1], g2 = gray[(size_t)y2 * g.W + x2];
-          if (g1 < g2) continue;
+          const bool in = !(x1 < 0 || x1 >= g.W || y1 < 0 || y1 >= g.H) && !(x2 < 0 || x2 >= g.W || y2 < 0 || y2 >= g.H);
+          g1v[k] = -1;
+          g2v[k] = 0;
+          if (in) {
+            g1v[k] = gray[y1 * g.W + x1];
+            g2v[k] = gray[y2 * g.W + x2];
+          }
+        }
+        double Mn = 0, Mcount = 0;
+#pragma unroll
+        for (int k = 0; k < kSteps; k++) {
+          const double nn = -3.0 + 0.25 * k;
+          const int g1 = g1v[k], g2 = g2v[k];
+          if (g1 < g2) continue;  // also skips out-of-image steps (g1 = -1)
           const double weight = (double)((g2 - g1) * (g2 - g1));
           Mn += weight * nn;
           Mcount += weight;
@@ -1764,6 +2154,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         S.sy[t] = by;
       }
       __syncthreads();
+      phase(1);
       if (tid < 4) {
         double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
         const int o = S.samp_off[tid];
@@ -1781,6 +2172,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         S.lines[tid][3] = (double)det_sinf((float)nt);
       }
       __syncthreads();
+      phase(2);
       if (tid == 0) {
         float qp[4][2];
         for (int k = 0; k < 4; k++) { qp[k][0] = S.qc[k][0]; qp[k][1] = S.qc[k][1]; }
@@ -1803,38 +2195,26 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         for (int k = 0; k < 4; k++) { S.qc[k][0] = qp[k][0]; S.qc[k][1] = qp[k][1]; }
       }
       __syncthreads();
+      phase(3);
     }
     if (prm.diag_stop == 6) continue;
     // ---- homography (quad_update_homographies / homography_compute2) -----------
+    if (homography_wave(S.qc, S.A, S.H) != 0) continue;
     if (tid == 0) {
-      double corr[4][4];
-      for (int i = 0; i < 4; i++) {
-        corr[i][0] = (i == 0 || i == 3) ? -1 : 1;
-        corr[i][1] = (i == 0 || i == 1) ? -1 : 1;
-        corr[i][2] = S.qc[i][0];
-        corr[i][3] = S.qc[i][1];
-      }
-      double H[9];
-      int okh = homography_compute2(corr, H) == 0;
-      if (okh) {
-        const double hdet = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
-                            H[2] * (H[3] * H[7] - H[4] * H[6]);
-        okh = hdet != 0;
-      }
-      for (int k = 0; k < 9; k++) S.H[k] = H[k];
-      S.ok = okh;
+      const double* H = S.H;
+      const double hdet = H[0] * (H[4] * H[8] - H[5] * H[7]) - H[1] * (H[3] * H[8] - H[5] * H[6]) +
+                          H[2] * (H[3] * H[7] - H[4] * H[6]);
+      S.ok = hdet != 0;
     }
     __syncthreads();
+    phase(4);
     if (!S.ok) continue;
     // ---- quad_decode: border gray models (8 patterns x 8 samples = 64 lanes) ----
     {
       const int pidx = tid >> 3, i = tid & 7;
-      const float wab = 8.0f;
-      const float pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0, 1, 0}, {wab + 0.5f, .5f, 0, 1, 1},
-                               {wab - 0.5f, .5f, 0, 1, 0}, {0.5f, -0.5f, 1, 0, 1}, {0.5f, 0.5f, 1, 0, 0},
-                               {0.5f, wab + 0.5f, 1, 0, 1}, {0.5f, wab - 0.5f, 1, 0, 0}};
-      const double tagx01 = (double)((pat[pidx][0] + (float)i * pat[pidx][2]) / 8.0f);
-      const double tagy01 = (double)((pat[pidx][1] + (float)i * pat[pidx][3]) / 8.0f);
+      const float* pat = c_border_pat[pidx];
+      const double tagx01 = (double)((pat[0] + (float)i * pat[2]) / 8.0f);
+      const double tagy01 = (double)((pat[1] + (float)i * pat[3]) / 8.0f);
       const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
       double px, py;
       hproject(S.H, tagx, tagy, &px, &py);
@@ -1846,24 +2226,40 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     }
     for (int t = tid; t < 100; t += kDecodeThreads) S.values[t] = 0;
     __syncthreads();
-    if (tid == 0) {
-      GrayModel wm, bm;
+    phase(5);
+    // lane 0 builds and solves the white model, lane 1 the black one, each over
+    // its 32 samples in the serial order, eight samples staged in registers at a time
+    double interp00 = 0;
+    if (tid < 2) {
+      GrayModel m;
       for (int k = 0; k < 3; k++) {
-        wm.B[k] = bm.B[k] = 0;
-        for (int j = 0; j < 3; j++) wm.A[k][j] = bm.A[k][j] = 0;
+        m.B[k] = 0;
+        for (int j = 0; j < 3; j++) m.A[k][j] = 0;
       }
-      for (int t = 0; t < 64; t++) {
-        if (!S.gmvalid[t]) continue;
-        if (((t >> 3) & 1) == 0) gm_add(wm, S.gmx[t], S.gmy[t], S.gmv[t]);
-        else gm_add(bm, S.gmx[t], S.gmy[t], S.gmv[t]);
+      for (int grp = 0; grp < 4; grp++) {
+        const int t0 = 16 * grp + 8 * tid;
+        double xs[8], ys[8], vs[8];
+        int ok[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          xs[i] = S.gmx[t0 + i];
+          ys[i] = S.gmy[t0 + i];
+          vs[i] = S.gmv[t0 + i];
+          ok[i] = S.gmvalid[t0 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (ok[i]) gm_add(m, xs[i], ys[i], vs[i]);
       }
-      gm_solve(wm);
-      gm_solve(bm);
-      S.ok = !(gm_interp(wm, 0, 0) - gm_interp(bm, 0, 0) < 0);
-      for (int k = 0; k < 3; k++) { S.wC[k] = wm.C[k]; S.bC[k] = bm.C[k]; }
+      gm_solve(m);
+      double* C = tid == 0 ? S.wC : S.bC;
+      for (int k = 0; k < 3; k++) C[k] = m.C[k];
+      interp00 = gm_interp(m, 0, 0);
     }
+    const double w00 = __shfl(interp00, 0), b00 = __shfl(interp00, 1);
     __syncthreads();
-    if (!S.ok) continue;
+    if (w00 - b00 < 0) continue;  // uniform
+    phase(6);
     if (tid < 36) {
       const int bity = c_bity[tid], bitx = c_bitx[tid];
       const double tagx01 = (bitx + 0.5) / 8, tagy01 = (bity + 0.5) / 8;
@@ -1883,6 +2279,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       }
     }
     __syncthreads();
+    phase(7);
     // sharpen (apriltag.c): each lane owns cells t, t+64
     double shv[2];
     for (int r = 0; r < 2; r++) {
@@ -1919,6 +2316,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       S.margin = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
     }
     __syncthreads();
+    phase(8);
     // quick_decode_codeword: first rotation, then entry, within hamming <= 2
     uint32_t bc = 0xffffffffu;
     {
@@ -1941,10 +2339,8 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         d.id = c_book.id[ent];
         d.hamming = hd;
         d.decision_margin = margin;
-        d.blob_rank = (int32_t)qd.rank;
-        const double kRotC[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
-        const double kRotS[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
-        const double R[9] = {kRotC[rot], -kRotS[rot], 0, kRotS[rot], kRotC[rot], 0, 0, 0, 1};
+        d.blob_rank = (int32_t)qrank;
+        const double R[9] = {c_rot_c[rot], -c_rot_s[rot], 0, c_rot_s[rot], c_rot_c[rot], 0, 0, 0, 1};
         for (int i = 0; i < 3; i++)
           for (int j = 0; j < 3; j++) {
             double acc = 0;
@@ -1963,7 +2359,9 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       }
     }
     __syncthreads();
+    phase(9);
   }
+  probe_flush(b, prm, pacc, 128, tid == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2054,16 +2452,27 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   hipLaunchKernelGGL(k_group, dim3(std::max(32, std::min(512, 1024 / B)), B), dim3(256), 0, st, b, g);
   tk(6, st, 1);
   mark();
+  tk(7, st, 0);
+  hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
+  tk(7, st, 1);
+  mark();
   auto blob_large = [&](hipStream_t s) {
-    tk(8, s, 0);
-    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_blob<1024>, dim3(nblobwg), dim3(1024), 0, s, b, g, prm);
-    else hipLaunchKernelGGL(k_blob<256>, dim3(nblobwg), dim3(256), 0, s, b, g, prm);
-    tk(8, s, 1);
+    tk(9, s, 0);
+    // LDS sized for the largest blob the geometry admits (max_cluster = 2 (W + H))
+    const bool cap4k = g.max_cluster <= 4096;
+    if (B < kWideBlobMaxBatch) {
+      if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+      else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+    } else {
+      if (cap4k) hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm);
+      else hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(nblobwg), dim3(256), 0, s, b, g, prm);
+    }
+    tk(9, s, 1);
   };
   auto blob_small = [&](hipStream_t s) {
-    tk(7, s, 0);
+    tk(8, s, 0);
     hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
-    tk(7, s, 1);
+    tk(8, s, 1);
   };
   if (ev || !st2) {
     blob_small(st);
@@ -2079,13 +2488,13 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }
-  tk(9, st, 0);
-  hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm);
-  tk(9, st, 1);
-  mark();
   tk(10, st, 0);
-  if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
+  hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm, B);
   tk(10, st, 1);
+  mark();
+  tk(11, st, 0);
+  if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
+  tk(11, st, 1);
   mark();
   return hipGetLastError();
 }

@@ -71,5 +71,7 @@ def test_family_matches_oracle(oracle_mod):
 def test_stage_names():
     from ros_vision_amd import detector
     L = detector.load_library()
-    names = [L.at_stage_name(i).decode() for i in range(9)]
-    assert names[0] == "k_pre" and "k_blob" in names and L.at_stage_name(99) == b""
+    names = [L.at_stage_name(i).decode() for i in range(32)]
+    names = names[:names.index("")]
+    assert names[0] == "k_pre" and names[-1] == "k_pose" and L.at_stage_name(99) == b""
+    assert {"k_extents", "k_blob_small", "k_blob", "k_decode"} <= set(names)

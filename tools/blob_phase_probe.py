@@ -1,4 +1,4 @@
-"""Accumulated per-phase time of the blob kernels (AT_PHASE_PROBE=1): phase k
+"""Accumulated per-phase time of the blob and decode kernels (AT_PHASE_PROBE=1): phase k
 of blob_item = time from marker k-1 to marker k summed over all work items
 (microseconds of wave time), for the wave-per-blob (small) and the
 workgroup-per-blob (large) variants."""
@@ -22,9 +22,13 @@ det.detect_device(d_frames.data_ptr(), frames[0].nbytes, B)
 p0 = det.copy_probe().astype(np.int64)
 det.detect_device(d_frames.data_ptr(), frames[0].nbytes, B)
 p = det.copy_probe().astype(np.int64) - p0
-names = {0: "extents+select", 1: "(diag1)", 2: "theta+sort", 3: "prefix sums", 4: "errors+filter",
-         7: "peaks", 8: "fitquads", 9: "update+emit"}
-for kind, base in (("small", 64), ("large", 80)):
+names = {0: "select check", 1: "load keys", 2: "theta sort", 3: "compact+scan", 4: "errors",
+         5: "filter+peaks", 6: "top10+prefix", 7: "segment fits", 8: "combinations", 9: "update+emit"}
+dnames = {1: "refine samples", 2: "edge fits", 3: "corners", 4: "homography", 5: "gray samples",
+          6: "gray models", 7: "bit samples", 8: "sharpen+score", 9: "codebook+emit"}
+for kind, base in (("small", 64), ("large", 80), ("decode", 128)):
+    if kind == "decode":
+        names = dnames
     print(kind)
     for k in range(16):
         if p[base + k] or p[base + 32 + k]:
