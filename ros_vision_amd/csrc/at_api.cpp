@@ -190,6 +190,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.CTX = (g.Wd + kCclTile - 1) / kCclTile;
   g.CTY = (g.Hd + kCclTile - 1) / kCclTile;
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
+  g.BTX = (g.Wd - 2 + 63) / 64;
+  g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
+  g.ntb = g.BTX * g.BTY;
   g.min_cluster = (uint32_t)std::max(24, cfg->min_cluster_pixels);
   g.max_cluster = (uint32_t)(2 * (W + H));
   g.min_tag_width = std::max(3, 8 / 2);  // tag36h11 width_at_border 8 / quad_decimate 2
@@ -252,10 +255,15 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.par = (uint32_t*)dalloc(B * nd * 4);
   b.lab = (uint32_t*)dalloc(B * nd * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
-  b.pts = (uint64_t*)dalloc(B * g.cap_pts * 8);
+  const size_t ntb = (size_t)g.ntb;
+  b.pts = (uint64_t*)dalloc(B * ntb * kBndPts * 8);
+  b.tcnt = (uint32_t*)dalloc(B * ntb * 4);
+  b.tent = (uint32_t*)dalloc(B * ntb * 4);
   b.grp = (uint64_t*)dalloc(B * g.cap_pts * 8);
-  b.pent_key = (uint64_t*)dalloc(B * kPairEntCap * 8);
-  b.pent_cnt = (uint32_t*)dalloc(B * kPairEntCap * 4);
+  b.pent_key = (uint64_t*)dalloc(B * ntb * kLdsPairSlots * 8);
+  b.pent_cnt = (uint32_t*)dalloc(B * ntb * kLdsPairSlots * 4);
+  b.povf_key = (uint64_t*)dalloc(B * kPairEntCap * 8);
+  b.povf_cnt = (uint32_t*)dalloc(B * kPairEntCap * 4);
   b.ht_key = (uint64_t*)dalloc(B * kHashSlots * 8);
   b.ht_cnt = (uint32_t*)dalloc(B * kHashSlots * 4);
   b.ht_rank = (uint32_t*)dalloc(B * kHashSlots * 4);
@@ -680,10 +688,23 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       return (long long)need;
     }
     case AT_STAGE_POINTS: {
-      const uint32_t np = std::min<uint32_t>(d->h_ctrl[kCtlNpts * B + frame], (uint32_t)g.cap_pts);
-      src = d->d.pts + (size_t)frame * g.cap_pts;
-      n = (size_t)np * 8;
-      break;
+      // the tiles' regions concatenated in tile order
+      const size_t ntb = (size_t)g.ntb;
+      std::vector<uint32_t> tc(ntb);
+      std::vector<uint64_t> all(ntb * kBndPts);
+      if (hipMemcpy(tc.data(), d->d.tcnt + frame * ntb, ntb * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(all.data(), d->d.pts + frame * ntb * kBndPts, all.size() * 8, hipMemcpyDeviceToHost) !=
+              hipSuccess)
+        return AT_E_HIP;
+      size_t np = 0;
+      for (size_t t = 0; t < ntb; t++) np += tc[t];
+      if (bytes < np * 8) return AT_E_INVALID;
+      size_t o = 0;
+      for (size_t t = 0; t < ntb; t++) {
+        memcpy((uint8_t*)dst + o * 8, all.data() + t * kBndPts, tc[t] * 8);
+        o += tc[t];
+      }
+      return (long long)(np * 8);
     }
     case AT_STAGE_BLOB_POINTS: {
       // IndexPoint keys of the selected pairs, in rank order

@@ -12,7 +12,12 @@ namespace at {
 constexpr int kCclTile = 32;           // CCL tile edge in decimated pixels (16x16 2x2-blocks)
 constexpr int kHashSlots = 8192;       // per-frame open-addressing table of blob pairs (<= 50% full)
 constexpr int kHashBits = 13;
-constexpr int kPairEntCap = 65536;     // per-frame (tile, pair, count) entries k_boundary hands to k_pairs
+constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count) entries (tiles with > kLdsPairSlots pairs)
+// k_boundary tiles: 64 x (4 * kBndRows) interior pixels per 256-thread workgroup;
+// each tile owns a fixed region of kBndPts points and kLdsPairSlots pair entries
+constexpr int kBndRows = 4;
+constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel
+constexpr int kLdsPairSlots = 512;
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kMaxDets = 128;          // candidate detections per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
@@ -52,6 +57,7 @@ struct Geom {
   int BW, BH;           // 2x2 CCL blocks
   int CTX, CTY;         // CCL tiles
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)
+  int BTX, BTY, ntb;    // k_boundary tiles (64 x 4*kBndRows interior pixels each)
   uint32_t min_cluster; // max(24, min_cluster_pixels)
   uint32_t max_cluster; // 2 * (W + H)
   int min_tag_width;    // width_at_border / quad_decimate, >= 3
@@ -113,11 +119,15 @@ struct DevBufs {
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
   uint32_t* lab;      // [B][Wd*Hd]
   uint32_t* size;     // [B][Wd*Hd]
-  uint64_t* pts;      // [B][cap_pts]   boundary points, emission order
+  uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
+  uint32_t* tcnt;     // [B][ntb]        points of each tile
+  uint32_t* tent;     // [B][ntb]        pair entries of each tile
   uint64_t* grp;      // [B][cap_pts]   boundary points grouped by pair rank
-  uint64_t* pent_key; // [B][kPairEntCap]  per-tile pair histogram entries (rep01)
-  uint32_t* pent_cnt; // [B][kPairEntCap]
-  uint32_t* npent;    // [B] (in the control block)
+  uint64_t* pent_key; // [B][ntb][kLdsPairSlots] per-tile pair histogram entries (rep01)
+  uint32_t* pent_cnt; // [B][ntb][kLdsPairSlots]
+  uint64_t* povf_key; // [B][kPairEntCap] entries of tiles whose LDS pair table overflowed
+  uint32_t* povf_cnt; // [B][kPairEntCap]
+  uint32_t* npent;    // [B] (control block) overflow entries; k_pairs then stores the frame's total entries
   uint64_t* ht_key;   // [B][kHashSlots]  written whole by k_pairs
   uint32_t* ht_cnt;   // [B][kHashSlots]
   uint32_t* ht_rank;  // [B][kHashSlots]

@@ -465,8 +465,6 @@ __device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
   return 1 + (uint32_t)__builtin_ctzll(rest);
 }
 
-constexpr int kLdsPairSlots = 512;
-
 __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uint64_t key, uint32_t len) {
   uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
   for (int probe = 0; probe < kLdsPairSlots; probe++) {
@@ -492,14 +490,12 @@ __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uin
 // ONE global atomic per workgroup; the pair histogram is aggregated in an LDS
 // hash table (runs of equal pairs in consecutive lanes first) and appended to
 // the frame's pair-entry list with one more global atomic per workgroup.
-constexpr int kBndRows = 4;
-constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel
 
 __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key, uint32_t cnt) {
   const uint32_t o = atomicAdd(b.npent + f, 1u);
   if (o < (uint32_t)kPairEntCap) {
-    b.pent_key[(size_t)f * kPairEntCap + o] = key;
-    b.pent_cnt[(size_t)f * kPairEntCap + o] = cnt;
+    b.povf_key[(size_t)f * kPairEntCap + o] = key;
+    b.povf_cnt[(size_t)f * kPairEntCap + o] = cnt;
   } else {
     atomicOr(b.status + f, kStatusHashFull);
   }
@@ -509,7 +505,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
   __shared__ uint64_t s_pts[kBndPts];
-  __shared__ uint32_t s_npts, s_nent, s_base, s_ebase;
+  __shared__ uint32_t s_npts, s_nent;
   __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
   __shared__ uint8_t s_tbig[(4 * kBndRows + 1) * 66];
   __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
@@ -606,37 +602,27 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       if (pk[dir]) s_pts[pos++] = pk[dir];
   }
   __syncthreads();
+  // the tile's own regions: points and compacted pair entries, plain stores
+  // (no per-frame counter: a device-scope atomic per tile on a per-frame
+  // address serialized the tiles of a frame)
   const uint32_t total = s_npts;
-  if (tid == 0) s_base = total ? atomicAdd(b.npts + f, total) : 0u;
-  // count the distinct pairs of the tile
-  uint32_t mine = 0;
-  for (int i = tid; i < kLdsPairSlots; i += 256) mine += s_pkey[i] != 0;
-  uint32_t wn = mine;
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) wn += __shfl_xor(wn, d);
-  if (lane == 0 && wn) atomicAdd(&s_nent, wn);
-  __syncthreads();
-  const uint32_t nent = s_nent;
-  if (tid == 0) s_ebase = nent ? atomicAdd(b.npent + f, nent) : 0u;
-  if (tid == 0) s_nent = 0;
-  __syncthreads();
-  const uint32_t base = s_base, ebase = s_ebase;
-  uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
-  for (uint32_t i = tid; i < total; i += 256) {
-    if (base + i < (uint32_t)g.cap_pts) pts[base + i] = s_pts[i];
-    else atomicOr(b.status + f, kStatusPointsOverflow);
-  }
+  const size_t tb = (size_t)f * g.ntb + blockIdx.y * gridDim.x + blockIdx.x;
+  uint64_t* pts = b.pts + tb * kBndPts;
+  for (uint32_t i = tid; i < total; i += 256) pts[i] = s_pts[i];
+  uint64_t* ekey = b.pent_key + tb * kLdsPairSlots;
+  uint32_t* ecnt = b.pent_cnt + tb * kLdsPairSlots;
   for (int i = tid; i < kLdsPairSlots; i += 256) {
     const uint64_t k = s_pkey[i];
     if (k) {
-      const uint32_t o = ebase + atomicAdd(&s_nent, 1u);
-      if (o < (uint32_t)kPairEntCap) {
-        b.pent_key[(size_t)f * kPairEntCap + o] = k;
-        b.pent_cnt[(size_t)f * kPairEntCap + o] = s_pcnt[i];
-      } else {
-        atomicOr(b.status + f, kStatusHashFull);
-      }
+      const uint32_t o = atomicAdd(&s_nent, 1u);
+      ekey[o] = k;
+      ecnt[o] = s_pcnt[i];
     }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    b.tcnt[tb] = total;
+    b.tent[tb] = s_nent;
   }
 }
 
@@ -687,19 +673,17 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __shared__ uint32_t t_cnt[kHashSlots];
   __shared__ uint64_t s_list[kMaxPairs];
   __shared__ uint32_t s_cnt[kMaxPairs];
-  __shared__ uint32_t s_n, s_full;
+  __shared__ uint32_t s_n, s_full, s_np, s_ne;
   __shared__ uint32_t s_wsum[16];
   for (int i = tid; i < kHashSlots; i += 1024) {
     t_key[i] = 0;
     t_cnt[i] = 0;
   }
-  if (tid == 0) { s_n = 0; s_full = 0; }
+  if (tid == 0) { s_n = 0; s_full = 0; s_np = 0; s_ne = 0; }
   __syncthreads();
-  // merge the per-tile pair histograms of k_boundary in LDS
-  const uint32_t total = min(b.npent[f], (uint32_t)kPairEntCap);
-  for (uint32_t i = tid; i < total; i += 1024) {
-    const uint64_t key = b.pent_key[(size_t)f * kPairEntCap + i];
-    const uint32_t cnt = b.pent_cnt[(size_t)f * kPairEntCap + i];
+  // merge the per-tile pair histograms of k_boundary in LDS: wave w takes
+  // tiles w, w + 16, ...; then the overflow entries of crowded tiles
+  auto merge = [&](uint64_t key, uint32_t cnt) {
     uint32_t h = (uint32_t)mix_hash(key);
     bool done = false;
     for (int probe = 0; probe < kHashSlots && !done; probe++) {
@@ -717,6 +701,25 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       h = (h + 1) & (kHashSlots - 1);
     }
     if (!done) s_full = 1;
+  };
+  {
+    const uint32_t lane = lane_id();
+    uint32_t np = 0, ne = 0;
+    for (int t = tid >> 6; t < g.ntb; t += 16) {
+      const size_t tb = (size_t)f * g.ntb + t;
+      const uint32_t nt = b.tent[tb];
+      if (lane == 0) { np += b.tcnt[tb]; ne += nt; }
+      for (uint32_t j = lane; j < nt; j += 64) merge(b.pent_key[tb * kLdsPairSlots + j], b.pent_cnt[tb * kLdsPairSlots + j]);
+    }
+    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
+    for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
+    if (lane == 0 && np) atomicAdd(&s_np, np);
+    if (lane == 0 && ne) atomicAdd(&s_ne, ne);
+    __syncthreads();
+    if (tid == 0) {
+      b.npts[f] = s_np;            // boundary points of the frame (N_c)
+      b.npent[f] = s_ne + novf;    // entries merged (diagnostic)
+    }
   }
   __syncthreads();
   stamp(1);
@@ -826,34 +829,62 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 // ---------------------------------------------------------------------------
 // K8: scatter the points into their pair segments (grouped by pair rank).
 // ---------------------------------------------------------------------------
+// One workgroup per k_boundary tile: every (tile, pair) entry reserves its
+// points' range of the pair segment with one atomic, then the tile's points
+// take consecutive slots of their entry (LDS cursor).  Pairs missing from the
+// tile's entries (LDS table overflow in k_boundary) reserve per point.
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const int f = blockIdx.y;
   if (b.status[f] & (kStatusPairsOverflow | kStatusHashFull)) return;
-  const uint32_t n = b.npts[f];
-  const uint64_t* pts = b.pts + (size_t)f * g.cap_pts;
-  uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
+  __shared__ uint64_t s_hk[2 * kLdsPairSlots];
+  __shared__ uint32_t s_he[2 * kLdsPairSlots];
+  __shared__ uint32_t s_base[kLdsPairSlots], s_cur[kLdsPairSlots];
+  const int tid = threadIdx.x;
+  const size_t tb = (size_t)f * g.ntb + blockIdx.x;
+  const uint32_t n = b.tcnt[tb], ne = b.tent[tb];
   const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
   const uint32_t* ht_off = b.ht_off + (size_t)f * kHashSlots;
   uint32_t* ht_cur = b.ht_cur + (size_t)f * kHashSlots;
-  const uint32_t lane = lane_id();
-  const uint32_t stride = gridDim.x * 256;
-  const uint32_t nround = (n + stride - 1) / stride;
-  for (uint32_t r = 0; r < nround; r++) {
-    const uint32_t i = r * stride + blockIdx.x * 256 + threadIdx.x;
-    const bool has = i < n;
-    const uint64_t key = has ? pts[i] : 0;
+  for (int i = tid; i < 2 * kLdsPairSlots; i += 256) s_hk[i] = 0;
+  __syncthreads();
+  for (uint32_t e = tid; e < ne; e += 256) {
+    const uint64_t key = b.pent_key[tb * kLdsPairSlots + e];
+    const uint32_t cnt = b.pent_cnt[tb * kLdsPairSlots + e];
+    const uint32_t slot = ht_slot_find(ht_key, key);
+    s_base[e] = slot == 0xffffffffu ? 0u : ht_off[slot] + atomicAdd(ht_cur + slot, cnt);
+    s_cur[e] = 0;
+    uint32_t h = (uint32_t)(mix_hash(key) & (2 * kLdsPairSlots - 1));
+    while (true) {  // keys are distinct and the table is at most half full
+      const uint64_t prev = atomicCAS((unsigned long long*)&s_hk[h], 0ull, (unsigned long long)key);
+      if (prev == 0) {
+        s_he[h] = e;
+        break;
+      }
+      h = (h + 1) & (2 * kLdsPairSlots - 1);
+    }
+  }
+  __syncthreads();
+  const uint64_t* pts = b.pts + tb * kBndPts;
+  uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint64_t key = pts[i];
     const uint64_t r01 = key >> 24;
-    const uint32_t slot = has ? ht_slot_find(ht_key, r01) : 0xffffffffu;
-    const uint32_t prev = __shfl_up(slot, 1);
-    const bool same = has && lane > 0 && prev == slot;
-    const uint64_t same_mask = __ballot(same);
-    const uint64_t head_mask = __ballot(has && !same);
-    uint32_t base = 0;
-    if (has && !same) base = atomicAdd(ht_cur + slot, run_len(same_mask, lane));
-    const uint64_t upto = head_mask & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
-    const uint32_t head = upto ? 63 - __clzll(upto) : 0;
-    const uint32_t hb = __shfl(base, head);
-    if (has) grp[ht_off[slot] + hb + (lane - head)] = key;
+    uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kLdsPairSlots - 1));
+    uint32_t e = 0xffffffffu;
+    for (int probe = 0; probe < 2 * kLdsPairSlots; probe++) {
+      const uint64_t k = s_hk[h];
+      if (k == r01) { e = s_he[h]; break; }
+      if (k == 0) break;
+      h = (h + 1) & (2 * kLdsPairSlots - 1);
+    }
+    uint32_t pos;
+    if (e != 0xffffffffu) {
+      pos = s_base[e] + atomicAdd(&s_cur[e], 1u);
+    } else {
+      const uint32_t slot = ht_slot_find(ht_key, r01);
+      pos = ht_off[slot] + atomicAdd(ht_cur + slot, 1u);
+    }
+    grp[pos] = key;
   }
 }
 
@@ -2438,7 +2469,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     mark();
   }
   {
-    dim3 blk(64, 4), grd((g.Wd - 2 + 63) / 64, (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows), B);
+    dim3 blk(64, 4), grd(g.BTX, g.BTY, B);
     tk(4, st, 0);
     hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
     tk(4, st, 1);
@@ -2449,7 +2480,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(5, st, 1);
   mark();
   tk(6, st, 0);
-  hipLaunchKernelGGL(k_group, dim3(std::max(32, std::min(512, 1024 / B)), B), dim3(256), 0, st, b, g);
+  hipLaunchKernelGGL(k_group, dim3(g.ntb, B), dim3(256), 0, st, b, g);
   tk(6, st, 1);
   mark();
   tk(7, st, 0);
