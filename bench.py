@@ -6,8 +6,10 @@ on N MI355X (BASELINE.json metric; workload = configs[1], a single-camera
 A *step* is one launch sequence over a batch of B frames that are already
 resident in HBM (see DESIGN.md "Measurement").  Each rank owns its own shard of
 the stream (weak scaling, no data-path collective: frames are independent).
-Two detector instances on two HIP streams are used round-robin so the host
-tail (reconcile + sort by id) of batch k overlaps the kernels of batch k+1.
+Four detector instances (one HIP stream and hardware queue each) are used
+round-robin, so up to four batches are in flight: the latency-bound kernels of
+one batch overlap those of the others, and the host tail (reconcile + sort by
+id) of batch k overlaps the kernels of the later ones.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -45,8 +47,11 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--tags", type=int, default=15)
     ap.add_argument("--latency-frames", type=int, default=200)
-    ap.add_argument("--instances", type=int, default=2,
+    ap.add_argument("--instances", type=int, default=4,
                     help="detector instances (one HIP stream each) used round-robin, i.e. batches in flight")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
+                         "detector stream so the batches in flight run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
     ap.add_argument("--ingest", choices=["local", "scatter"], default="local",
@@ -65,12 +70,13 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
         return nf * (2 * W * H + W * H + Wd * Hd)           # YUYV in, gray + decimated out
     if kernel == "k_boundary":
         return nf * 5 * Wd * Hd + 8 * stats.get("boundary_points", 0)  # thr + labels in, points out
-    if kernel == "k_blob":
-        return 12 * stats.get("large_blob_points", 0)      # 8-B point key + 4 gradient bytes per point
+    if kernel == "k_blob":  # kept blobs: 8-B sort key in + 4 gradient bytes per point
+        return 12 * stats.get("large_blob_points", 0)
     if kernel == "k_blob_small":
         return 12 * stats.get("small_blob_points", 0)
-    if kernel == "k_extents":  # candidate points read twice, kept points' sort keys written
-        return 24 * (stats.get("small_blob_points", 0) + stats.get("large_blob_points", 0))
+    if kernel == "k_extents":  # candidate points read (bounded by all boundary points), kept points' keys written
+        return 8 * stats.get("boundary_points", 0) + 8 * (stats.get("small_blob_points", 0) +
+                                                          stats.get("large_blob_points", 0))
     if kernel in ("k_thr_ccl", "k_ccl_final"):
         return nf * 9 * Wd * Hd                            # dec/thr in, labels/sizes out
     return None
@@ -124,6 +130,9 @@ def cpu_baseline(frames, width, height):
 
 def main():
     args = parse()
+    # several detector instances (batches in flight) each own a HIP stream: give the
+    # process one hardware queue per stream; must precede HIP runtime initialisation
+    os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     # stdout carries exactly one JSON line: libraries that print banners to fd 1
     # (RCCL prints its version block at communicator init) are sent to stderr
     json_out = os.fdopen(os.dup(1), "w")

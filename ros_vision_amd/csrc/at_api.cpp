@@ -193,6 +193,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.BTX = (g.Wd - 2 + 63) / 64;
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
   g.ntb = g.BTX * g.BTY;
+  if (g.ntb > kMaxTilesPerFrame) return AT_E_INVALID;
   g.min_cluster = (uint32_t)std::max(24, cfg->min_cluster_pixels);
   g.max_cluster = (uint32_t)(2 * (W + H));
   g.min_tag_width = std::max(3, 8 / 2);  // tag36h11 width_at_border 8 / quad_decimate 2
@@ -207,6 +208,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
   p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
+  p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) return AT_E_INVALID;
   p.tag_size = cfg->tag_size;
@@ -218,11 +220,13 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipSetDevice(d->device) != hipSuccess) return fail(AT_E_HIP);
   if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
-  // AT_NO_FORK=1: the two blob kernels run back to back on the one stream (more
-  // detector instances can then share the process's hardware queues)
-  if (!(getenv("AT_NO_FORK") && atoi(getenv("AT_NO_FORK"))) &&
-      hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess)
-    return fail(AT_E_HIP);
+  // Latency mode (max_batch < kWideBlobMaxBatch): the small-blob kernel runs on a
+  // second stream beside the large-blob one.  Throughput mode: both on the one
+  // stream -- concurrency comes from several detector instances (batches in
+  // flight), which then each need one hardware queue only.  AT_NO_FORK=1 forces
+  // the single-stream form.
+  const bool fork = d->B < kWideBlobMaxBatch && !(getenv("AT_NO_FORK") && atoi(getenv("AT_NO_FORK")));
+  if (fork && hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   d->kt.stage = -1;

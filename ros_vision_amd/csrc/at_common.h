@@ -18,6 +18,7 @@ constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count)
 constexpr int kBndRows = 4;
 constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel
 constexpr int kLdsPairSlots = 512;
+constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kMaxDets = 128;          // candidate detections per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
@@ -74,6 +75,7 @@ struct Params {
   double tag_size;  // metres; > 0 runs k_pose (apriltags_cuda_detector.hpp:39 TAGSIZE)
   int probe;      // diagnostics only (AT_PHASE_PROBE): kernels stamp phase clocks into DevBufs::probe
   int taps;       // write the sorted IndexPoint parity tap (AT_STAGE_BLOB_POINTS) over the grouped points
+  int wide_blob;  // AT_WIDE_BLOB=1: 512-thread large-blob teams at every batch size (experiment)
 };
 constexpr int kProbeWords = 256;
 

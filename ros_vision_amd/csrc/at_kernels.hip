@@ -42,6 +42,54 @@ __device__ __forceinline__ uint64_t mix_hash(uint64_t k) {
 __device__ __forceinline__ int dx_of(int dxy) { return dxy == 3 ? -1 : (dxy == 2 ? 0 : 1); }
 __device__ __forceinline__ int dy_of(int dxy) { return dxy == 0 ? 0 : 1; }
 
+// ---- block reductions (256 threads = 4 waves) ------------------------------
+template <typename T, typename Op>
+__device__ T wave_reduce(T v, Op op) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = op(v, __shfl_xor(v, d));
+  return v;
+}
+
+struct MinOp { template <typename T> __device__ T operator()(T a, T c) const { return a < c ? a : c; } };
+struct MaxOp { template <typename T> __device__ T operator()(T a, T c) const { return a > c ? a : c; } };
+struct AddOp { template <typename T> __device__ T operator()(T a, T c) const { return a + c; } };
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, Op op, T* s_tmp /* >= NW */, int NW) {
+  v = wave_reduce(v, op);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) s_tmp[w] = v;
+  __syncthreads();
+  T r = s_tmp[0];
+  for (int i = 1; i < NW; i++) r = op(r, s_tmp[i]);
+  return r;
+}
+
+// inclusive block scan of one value per thread (NW waves); returns the
+// inclusive prefix, *total = block sum
+template <typename T>
+__device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T u = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v = v + u;
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 63) s_tmp[w] = v;
+  __syncthreads();
+  T base = 0, tot = 0;
+  for (int i = 0; i < NW; i++) {
+    if (i < w) base = base + s_tmp[i];
+    tot = tot + s_tmp[i];
+  }
+  *total = tot;
+  return base + v;
+}
+
+
 struct DevCodebook {
   int n;
   uint64_t code[96];
@@ -703,22 +751,35 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     if (!done) s_full = 1;
   };
   {
-    const uint32_t lane = lane_id();
-    uint32_t np = 0, ne = 0;
-    for (int t = tid >> 6; t < g.ntb; t += 16) {
-      const size_t tb = (size_t)f * g.ntb + t;
-      const uint32_t nt = b.tent[tb];
-      if (lane == 0) { np += b.tcnt[tb]; ne += nt; }
-      for (uint32_t j = lane; j < nt; j += 64) merge(b.pent_key[tb * kLdsPairSlots + j], b.pent_cnt[tb * kLdsPairSlots + j]);
+    // tile entry counts -> exclusive prefix in LDS (one load round trip), then
+    // every entry of the frame in one flat pass
+    __shared__ uint32_t s_tpre[kMaxTilesPerFrame + 1];
+    const int ntb = g.ntb;
+    // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
+    const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
+    const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
+    uint32_t tot_e;
+    const uint32_t incl_e = block_incl_scan(ne, s_wsum, &tot_e, 16);
+    if (tid < ntb) s_tpre[tid] = incl_e - ne;
+    if (tid == 0) s_tpre[ntb] = tot_e;
+    if (np) atomicAdd(&s_np, np);
+    __syncthreads();
+    for (uint32_t i = tid; i < tot_e; i += 1024) {
+      int lo = 0, hi = ntb - 1;  // last tile whose prefix <= i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_tpre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      const size_t e = ((size_t)f * ntb + lo) * kLdsPairSlots + (i - s_tpre[lo]);
+      merge(b.pent_key[e], b.pent_cnt[e]);
     }
     const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
     for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
-    if (lane == 0 && np) atomicAdd(&s_np, np);
-    if (lane == 0 && ne) atomicAdd(&s_ne, ne);
     __syncthreads();
     if (tid == 0) {
-      b.npts[f] = s_np;            // boundary points of the frame (N_c)
-      b.npent[f] = s_ne + novf;    // entries merged (diagnostic)
+      b.npts[f] = s_np;           // boundary points of the frame (N_c)
+      b.npent[f] = tot_e + novf;  // entries merged (diagnostic)
     }
   }
   __syncthreads();
@@ -943,54 +1004,6 @@ __device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* e
   *err = (double)((float)m.N * eig);
   *mse = (double)eig;
 }
-
-// ---- block reductions (256 threads = 4 waves) ------------------------------
-template <typename T, typename Op>
-__device__ T wave_reduce(T v, Op op) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v = op(v, __shfl_xor(v, d));
-  return v;
-}
-
-struct MinOp { template <typename T> __device__ T operator()(T a, T c) const { return a < c ? a : c; } };
-struct MaxOp { template <typename T> __device__ T operator()(T a, T c) const { return a > c ? a : c; } };
-struct AddOp { template <typename T> __device__ T operator()(T a, T c) const { return a + c; } };
-
-template <typename T, typename Op>
-__device__ T block_reduce(T v, Op op, T* s_tmp /* >= NW */, int NW) {
-  v = wave_reduce(v, op);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane_id() == 0) s_tmp[w] = v;
-  __syncthreads();
-  T r = s_tmp[0];
-  for (int i = 1; i < NW; i++) r = op(r, s_tmp[i]);
-  return r;
-}
-
-// inclusive block scan of one value per thread (NW waves); returns the
-// inclusive prefix, *total = block sum
-template <typename T>
-__device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T u = __shfl_up(v, d);
-    if (lane >= (uint32_t)d) v = v + u;
-  }
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 63) s_tmp[w] = v;
-  __syncthreads();
-  T base = 0, tot = 0;
-  for (int i = 0; i < NW; i++) {
-    if (i < w) base = base + s_tmp[i];
-    tot = tot + s_tmp[i];
-  }
-  *total = tot;
-  return base + v;
-}
-
 
 // ---- team-generic primitives: a team is the whole 256-thread workgroup
 // (large blobs) or one 64-lane wave (small blobs, 4 independent teams per WG)
@@ -1301,10 +1314,13 @@ template <int CAP>
 constexpr int kPeakCap = (CAP / 4 * 4 > 3200 ? CAP / 4 * 4 : 3200) / 8;
 
 template <int NT, int CAP>
+constexpr int kKeySlots = CAP;
+
+template <int NT, int CAP>
 struct BlobShared {
-  uint64_t keys[CAP];
+  uint64_t keys[kKeySlots<NT, CAP>];
   union {
-    uint32_t bcnt[CAP / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
+    uint32_t bcnt[kKeySlots<NT, CAP> / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
     uint64_t peaks[kPeakCap<CAP>];
     struct {
       // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
@@ -1343,10 +1359,11 @@ constexpr uint64_t kThetaSpan = 50265600;  // > max theta = rint((2 pi) * 8e6)
 
 template <int NT, int CAP>
 __device__ bool team_bucket_sort(BlobShared<NT, CAP>& S, int n) {
-  if (n < 64 || 2 * n > CAP) return false;
+  constexpr int KEYS = kKeySlots<NT, CAP>;
+  if (n < 64 || 2 * n > KEYS) return false;
   const int tid = team_rank<NT>();
   int nb = 32;
-  while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= CAP/2
+  while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= KEYS/2
   auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> 23) * (uint64_t)nb) / kThetaSpan); };
   uint32_t* bcnt = S.u.bcnt;
   for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
@@ -1396,7 +1413,7 @@ __device__ bool team_bucket_sort(BlobShared<NT, CAP>& S, int n) {
     if ((b0 & 1) == 0) bcnt[b0 >> 1] = mine | (other << 16);
   }
   team_sync<NT>();
-  uint64_t* T = S.keys + CAP / 2;
+  uint64_t* T = S.keys + KEYS / 2;
   for (int t = tid; t < n; t += NT) {
     const uint64_t k = S.keys[t];
     const uint32_t bk = bucket(k);
@@ -1559,13 +1576,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   const int f = (int)(w >> 16);
   const uint32_t rank = w & 0xffff;
   const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
-  if (tid == 0) pacc[20] += n;  // points this team processed (batch statistics)
   const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
 
   // extents, SelectBlobs and the theta keys come from k_extents
   if (b.pair_sel[(size_t)f * kMaxPairs + rank] == 0) return;  // uniform across the team
+  if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
   const uint32_t bi = rank & 0xfff;
   phase(0);
   for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
@@ -2491,7 +2508,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(9, s, 0);
     // LDS sized for the largest blob the geometry admits (max_cluster = 2 (W + H))
     const bool cap4k = g.max_cluster <= 4096;
-    if (B < kWideBlobMaxBatch) {
+    if (B < kWideBlobMaxBatch || prm.wide_blob) {
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
     } else {
