@@ -257,7 +257,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.mm = (uint8_t*)dalloc(B * nt);
   b.thr = (uint8_t*)dalloc(B * nd);
   b.par = (uint32_t*)dalloc(B * nd * 4);
-  b.lab = (uint32_t*)dalloc(B * nd * 4);
+  b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodes * 4);
+  b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
   b.pts = (uint64_t*)dalloc(B * ntb * kBndPts * 8);
@@ -649,7 +650,34 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
     case AT_STAGE_GRAY: src = d->d.gray + frame * npix; n = npix; break;
     case AT_STAGE_DECIMATED: src = d->d.dec + frame * nd; n = nd; break;
     case AT_STAGE_THRESHOLD: src = d->d.thr + frame * nd; n = nd; break;
-    case AT_STAGE_LABELS: src = d->d.lab + frame * nd; n = nd * 4; break;
+    case AT_STAGE_LABELS: {
+      // LabelImage's output (labeling_allegretti_2019_BKE.cu:340-462) resolved
+      // from the union-find forest: label = par[par[node]] (node -> local root ->
+      // component root); 127 -> 0; a block of four 127 pixels -> the pixel index
+      if (bytes < nd * 4) return AT_E_INVALID;
+      std::vector<uint8_t> t(nd);
+      std::vector<uint32_t> par(nd);
+      if (hipMemcpy(t.data(), d->d.thr + frame * nd, nd, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(par.data(), d->d.par + frame * nd, nd * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return AT_E_HIP;
+      uint32_t* lab = (uint32_t*)dst;
+      const int Wd = g.Wd;
+      for (int y = 0; y < g.Hd; y++)
+        for (int x = 0; x < Wd; x++) {
+          const size_t i = (size_t)y * Wd + x;
+          const size_t F = (size_t)(y & ~1) * Wd + (x & ~1);
+          const bool all127 = t[F] == 127 && t[F + 1] == 127 && t[F + Wd] == 127 && t[F + Wd + 1] == 127;
+          if (all127) {
+            lab[i] = (uint32_t)i;
+          } else if (t[i] == 127) {
+            lab[i] = 0;
+          } else {
+            const size_t node = t[i] == 255 ? F : F + Wd + (x & 1);
+            lab[i] = par[par[node]];
+          }
+        }
+      return (long long)(nd * 4);
+    }
     case AT_STAGE_SIZES: src = d->d.size + frame * nd; n = nd * 4; break;
     case AT_STAGE_NUM_POINTS:
       if (bytes < 4) return AT_E_INVALID;

@@ -10,6 +10,7 @@ namespace at {
 
 // ---- capacities -----------------------------------------------------------
 constexpr int kCclTile = 32;           // CCL tile edge in decimated pixels (16x16 2x2-blocks)
+constexpr int kCclTileNodes = 768;     // union-find nodes of one CCL tile (3 per 2x2 block)
 constexpr int kHashSlots = 8192;       // per-frame open-addressing table of blob pairs (<= 50% full)
 constexpr int kHashBits = 13;
 constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count) entries (tiles with > kLdsPairSlots pairs)
@@ -32,7 +33,7 @@ constexpr int kNMaxima = 10;
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
 constexpr int kNumStages = 12;
-constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_final",
+constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_roots",
                                                  "k_boundary", "k_pairs", "k_group",     "k_extents",
                                                  "k_blob_small", "k_blob", "k_decode",   "k_pose"};
 
@@ -119,7 +120,8 @@ struct DevBufs {
   uint8_t* mm;        // [B][TW*TH*2]   unfiltered 4x4 min/max
   uint8_t* thr;       // [B][Wd*Hd]
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
-  uint32_t* lab;      // [B][Wd*Hd]
+  uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodes] local roots of each CCL tile (global node ids)
+  uint32_t* nlroot;   // [B][CTX*CTY]
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile

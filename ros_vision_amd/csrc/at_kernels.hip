@@ -230,9 +230,21 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
   __shared__ uint8_t s_t[33][36];  // thr of rows y0-1..y0+31, cols x0-1..x0+32 (+pad)
   __shared__ uint32_t s_par[768];
   __shared__ uint32_t s_cnt[768];
+  __shared__ uint32_t s_nlr;
+  if (tid == 0) s_nlr = 0;
 
   // unfiltered tile min/max for tile rows ty0-2..ty0+8, cols tx0-2..tx0+9
   const int ty0 = y0 / 4, tx0 = x0 / 4;
+  // the tile's decimated pixels (+1 halo) are loaded together with the tile
+  // min/max: one global round trip instead of two
+  constexpr int kDecPer = (33 * 34 + 255) / 256;
+  uint8_t dv[kDecPer];
+#pragma unroll
+  for (int k = 0; k < kDecPer; k++) {
+    const int i = tid + 256 * k;
+    const int y = y0 - 1 + i / 34, x = x0 - 1 + i % 34;
+    dv[k] = (i < 33 * 34 && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? dec[(size_t)y * g.Wd + x] : 0;
+  }
   for (int i = tid; i < 11 * 12; i += 256) {
     const int r = i / 12, c = i % 12;
     const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
@@ -262,21 +274,25 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
   }
   __syncthreads();
   // InternalThreshold for the 33x34 halo region; outside the image -> 127
-  for (int i = tid; i < 33 * 34; i += 256) {
-    const int r = i / 34, c = i % 34;
-    const int y = y0 - 1 + r, x = x0 - 1 + c;
-    uint8_t res = 127;
-    if (y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) {
-      const int fr = (y >> 2) - (ty0 - 1), fc = (x >> 2) - (tx0 - 1);
-      const int mn = s_fmn[fr][fc], mx = s_fmx[fr][fc];
-      if (mx - mn < prm.min_white_black_diff) {
-        res = 127;
-      } else {
-        const uint8_t th = (uint8_t)(mn + (mx - mn) / 2);
-        res = dec[(size_t)y * g.Wd + x] > th ? 255 : 0;
+#pragma unroll
+  for (int k = 0; k < kDecPer; k++) {
+    const int i = tid + 256 * k;
+    if (i < 33 * 34) {
+      const int r = i / 34, c = i % 34;
+      const int y = y0 - 1 + r, x = x0 - 1 + c;
+      uint8_t res = 127;
+      if (y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) {
+        const int fr = (y >> 2) - (ty0 - 1), fc = (x >> 2) - (tx0 - 1);
+        const int mn = s_fmn[fr][fc], mx = s_fmx[fr][fc];
+        if (mx - mn < prm.min_white_black_diff) {
+          res = 127;
+        } else {
+          const uint8_t th = (uint8_t)(mn + (mx - mn) / 2);
+          res = dv[k] > th ? 255 : 0;
+        }
       }
+      s_t[r][c] = res;
     }
-    s_t[r][c] = res;
   }
   for (int i = tid; i < 768; i += 256) {
     s_par[i] = i;
@@ -345,7 +361,15 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL), gid(rR));
     *reinterpret_cast<uint2*>(size + idF) = make_uint2(rF == F ? s_cnt[F] : 0u, 0u);
     *reinterpret_cast<uint2*>(size + idL) = make_uint2(rL == L ? s_cnt[L] : 0u, rR == R ? s_cnt[R] : 0u);
+    // the tile's local roots (components with pixels), for k_ccl_roots
+    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+    uint32_t* lr = b.lroot + tl * kCclTileNodes;
+    if (rF == F && s_cnt[F]) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
+    if (rL == L && s_cnt[L]) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
+    if (rR == R && s_cnt[R]) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
+  __syncthreads();
+  if (tid == 0) b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
 }
 
 // ---------------------------------------------------------------------------
@@ -424,59 +448,29 @@ __global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
 }
 
 // ---------------------------------------------------------------------------
-// K5: final labels (FinalLabeling, :340-462) and blob sizes.  One thread per
-// 2x2 block.  Local-root pixel counts move to the global root with one atomic
-// per local component instead of one per block.
+// K5: component roots and sizes (FinalLabeling, :340-462, for the roots only).
+// One wave per CCL tile, over the tile's local roots: find the global root
+// (the minimum node id of the component), point the local root straight at it
+// and move the local pixel count there.  Every node then reaches its label in
+// two hops -- node -> local root (k_thr_ccl) -> root -- which k_boundary
+// follows itself: there is no label plane.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t plain_find(const uint32_t* par, uint32_t n) {
-  uint32_t p = par[n];
-  while (p != n) {
-    n = p;
-    p = par[n];
-  }
-  return n;
-}
-
-__global__ __launch_bounds__(256) void k_ccl_final(DevBufs b, Geom g) {
-  const int f = blockIdx.z;
-  const int BX = blockIdx.x * 64 + threadIdx.x;
-  const int BY = blockIdx.y * 4 + threadIdx.y;
-  if (BX >= g.BW || BY >= g.BH) return;
+__global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
+  const int f = blockIdx.y;
+  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
-  const uint8_t* thr = b.thr + fo;
-  const uint32_t* par = b.par + fo;
-  uint32_t* lab = b.lab + fo;
+  uint32_t* par = b.par + fo;
   uint32_t* size = b.size + fo;
-  const int Wd = g.Wd;
-  const uint32_t idF = (uint32_t)(2 * BY * Wd + 2 * BX), idL = idF + Wd, idR = idL + 1;
-  const uint16_t top = *reinterpret_cast<const uint16_t*>(thr + idF);
-  const uint16_t bot = *reinterpret_cast<const uint16_t*>(thr + idL);
-  const uint8_t px[4] = {(uint8_t)(top & 0xff), (uint8_t)(top >> 8), (uint8_t)(bot & 0xff), (uint8_t)(bot >> 8)};
-  const bool any = px[0] != 127 || px[1] != 127 || px[2] != 127 || px[3] != 127;
-  if (!any) {
-    *reinterpret_cast<uint2*>(lab + idF) = make_uint2(idF, idF + 1);
-    *reinterpret_cast<uint2*>(lab + idL) = make_uint2(idL, idR);
-    return;
-  }
-  const uint32_t rF = plain_find(par, idF), rL = plain_find(par, idL), rR = plain_find(par, idR);
-  uint32_t l4[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    l4[k] = 0;
-    if (px[k] == 255) l4[k] = rF;
-    else if (px[k] == 0) l4[k] = (k == 0 || k == 2) ? rL : rR;
-  }
-  *reinterpret_cast<uint2*>(lab + idF) = make_uint2(l4[0], l4[1]);
-  *reinterpret_cast<uint2*>(lab + idL) = make_uint2(l4[2], l4[3]);
-  const uint32_t ids[3] = {idF, idL, idR}, roots[3] = {rF, rL, rR};
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    if (roots[k] != ids[k]) {
-      const uint32_t cnt = size[ids[k]];
-      if (cnt) {
-        atomicAdd(size + roots[k], cnt);
-        size[ids[k]] = 0;
-      }
+  const uint32_t n = b.nlroot[tl];
+  const uint32_t* lr = b.lroot + tl * kCclTileNodes;
+  for (uint32_t k = threadIdx.x; k < n; k += 64) {
+    const uint32_t l = lr[k];
+    const uint32_t r = g_find(par, l);
+    if (r != l) {
+      par[l] = r;  // unions are over: a concurrent find sees the old parent or r, both lead to r
+      const uint32_t cnt = size[l];
+      atomicAdd(size + r, cnt);  // result unused: no round trip
+      size[l] = 0;
     }
   }
 }
@@ -569,12 +563,14 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   // dependent global round trips per workgroup, then the point logic runs on LDS
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   const uint8_t* thr = b.thr + fo;
-  const uint32_t* lab = b.lab + fo;
+  const uint32_t* par = b.par + fo;
   const uint32_t* size = b.size + fo;
   const int Wd = g.Wd;
   const int ty0 = 1 + blockIdx.y * (4 * kBndRows), tx0 = blockIdx.x * 64;  // halo origin: x0 - 1
   constexpr int kTR = 4 * kBndRows + 1, kTC = 66, kTN = kTR * kTC;
   constexpr int kPer = (kTN + 255) / 256;
+  // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
+  // column) -> local root -> component root (k_ccl_roots)
   uint32_t lv[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
@@ -585,11 +581,16 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       const size_t i = (size_t)yy * Wd + xx;
       const uint32_t v = thr[i];
       s_tthr[e] = (uint8_t)v;
-      if (v != 127) lv[k] = lab[i];
+      const uint32_t F = (uint32_t)((yy & ~1) * Wd + (xx & ~1));
+      const uint32_t node = v == 255 ? F : F + Wd + (xx & 1);
+      if (v != 127) lv[k] = par[node];
     } else if (e < kTN) {
       s_tthr[e] = 127;
     }
   }
+#pragma unroll
+  for (int k = 0; k < kPer; k++)
+    if (lv[k] != 0xffffffffu) lv[k] = par[lv[k]];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
@@ -721,13 +722,13 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __shared__ uint32_t t_cnt[kHashSlots];
   __shared__ uint64_t s_list[kMaxPairs];
   __shared__ uint32_t s_cnt[kMaxPairs];
-  __shared__ uint32_t s_n, s_full, s_np, s_ne;
+  __shared__ uint32_t s_n, s_full, s_np;
   __shared__ uint32_t s_wsum[16];
   for (int i = tid; i < kHashSlots; i += 1024) {
     t_key[i] = 0;
     t_cnt[i] = 0;
   }
-  if (tid == 0) { s_n = 0; s_full = 0; s_np = 0; s_ne = 0; }
+  if (tid == 0) { s_n = 0; s_full = 0; s_np = 0; }
   __syncthreads();
   // merge the per-tile pair histograms of k_boundary in LDS: wave w takes
   // tiles w, w + 16, ...; then the overflow entries of crowded tiles
@@ -2478,13 +2479,10 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(2, st, 1);
     mark();
   }
-  {
-    dim3 blk(64, 4), grd((g.BW + 63) / 64, (g.BH + 3) / 4, B);
-    tk(3, st, 0);
-    hipLaunchKernelGGL(k_ccl_final, grd, blk, 0, st, b, g);
-    tk(3, st, 1);
-    mark();
-  }
+  tk(3, st, 0);
+  hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+  tk(3, st, 1);
+  mark();
   {
     dim3 blk(64, 4), grd(g.BTX, g.BTY, B);
     tk(4, st, 0);
