@@ -1926,61 +1926,96 @@ __device__ __forceinline__ bool work_item(const DevBufs& b, const uint32_t* cnt,
   return false;
 }
 
+// One candidate with a team of NT threads (a wave, or the whole workgroup for
+// large candidates); red: NT/64 x 8 LDS words for the cross-wave reduction.
+template <int NT>
+__device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, uint32_t w, int64_t (*red)[8]) {
+  const int tid = team_rank<NT>();
+  const int f = (int)(w >> 16);
+  const uint32_t rank = w & 0xffff;
+  const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
+  uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
+  int32_t sgx = 0, sgy = 0;
+  int64_t spg = 0;
+  for (uint32_t t = tid; t < n; t += NT) {
+    const uint64_t k = grp[t];
+    const int dxy = (int)(k & 3);
+    const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
+    const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
+    const bool b2w = (k & 8) != 0;
+    const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
+    mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
+    sgx += gx; sgy += gy;
+    spg += (int64_t)px * gx + (int64_t)py * gy;
+  }
+  mnx = wave_reduce(mnx, MinOp()); mxx = wave_reduce(mxx, MaxOp());
+  mny = wave_reduce(mny, MinOp()); mxy = wave_reduce(mxy, MaxOp());
+  sgx = wave_reduce(sgx, AddOp()); sgy = wave_reduce(sgy, AddOp());
+  spg = wave_reduce(spg, AddOp());
+  if constexpr (NT > 64) {
+    const int wv = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+      red[wv][0] = mnx; red[wv][1] = mxx; red[wv][2] = mny; red[wv][3] = mxy;
+      red[wv][4] = sgx; red[wv][5] = sgy; red[wv][6] = spg;
+    }
+    __syncthreads();
+    int32_t gx = 0, gy = 0;
+    int64_t pg = 0;
+    for (int i = 0; i < NT / 64; i++) {
+      mnx = min(mnx, (uint32_t)red[i][0]); mxx = max(mxx, (uint32_t)red[i][1]);
+      mny = min(mny, (uint32_t)red[i][2]); mxy = max(mxy, (uint32_t)red[i][3]);
+      gx += (int32_t)red[i][4]; gy += (int32_t)red[i][5]; pg += red[i][6];
+    }
+    sgx = gx; sgy = gy; spg = pg;
+    __syncthreads();  // red is reused by the next item
+  }
+  Ext e;
+  e.min_x = mnx; e.max_x = mxx; e.min_y = mny; e.max_y = mxy;
+  e.gx_sum = sgx; e.gy_sum = sgy; e.pg_sum = spg;
+  e.count = n;
+  bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
+  keep = keep && !((double)ext_dot(e) < 0.0);
+  if (!keep) return;  // uniform across the team
+  if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
+  const double cx = ext_cx(e), cy = ext_cy(e);
+  for (uint32_t t = tid; t < n; t += NT) {
+    const uint64_t k = grp[t];
+    const int dxy = (int)(k & 3);
+    const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
+    const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
+    const float dyf = (float)((double)py - cy);
+    const float dxf = (float)((double)px - cx);
+    const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
+    long long ti = (long long)rintf(theta);
+    if (ti < 0) ti = 0;
+    // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
+    grp[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
+             ((uint64_t)bx << 1) | ((k >> 3) & 1);
+  }
+}
+
+// Large candidates (size classes 0-2) one per workgroup, then small ones one
+// per wave.
 __global__ __launch_bounds__(256) void k_extents(DevBufs b, Geom g) {
-  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  const uint32_t lane = lane_id();
-  uint32_t cnt[kNumCls], total = 0;
+  __shared__ int64_t s_red[4][8];
+  uint32_t cnt[kNumCls], total = 0, nlarge = 0;
 #pragma unroll
   for (int c = 0; c < kNumCls; c++) {
     cnt[c] = min(b.ncls[c], b.wcap);
     total += cnt[c];
+    if (c < kNumLargeCls) nlarge += cnt[c];
   }
-  for (uint32_t it = gw; it < total; it += nw) {
+  for (uint32_t it = blockIdx.x; it < nlarge; it += gridDim.x) {
     uint32_t w = 0;
     work_item(b, cnt, 0, kNumCls, it, &w);
-    const int f = (int)(w >> 16);
-    const uint32_t rank = w & 0xffff;
-    const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
-    uint64_t* grp = b.grp + (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
-    uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
-    int32_t sgx = 0, sgy = 0;
-    int64_t spg = 0;
-    for (uint32_t t = lane; t < n; t += 64) {
-      const uint64_t k = grp[t];
-      const int dxy = (int)(k & 3);
-      const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
-      const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
-      const bool b2w = (k & 8) != 0;
-      const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
-      mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
-      sgx += gx; sgy += gy;
-      spg += (int64_t)px * gx + (int64_t)py * gy;
-    }
-    Ext e;
-    e.min_x = wave_reduce(mnx, MinOp()); e.max_x = wave_reduce(mxx, MaxOp());
-    e.min_y = wave_reduce(mny, MinOp()); e.max_y = wave_reduce(mxy, MaxOp());
-    e.gx_sum = wave_reduce(sgx, AddOp()); e.gy_sum = wave_reduce(sgy, AddOp());
-    e.pg_sum = wave_reduce(spg, AddOp());
-    e.count = n;
-    bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
-    keep = keep && !((double)ext_dot(e) < 0.0);
-    if (!keep) continue;  // uniform across the wave
-    if (lane == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
-    const double cx = ext_cx(e), cy = ext_cy(e);
-    for (uint32_t t = lane; t < n; t += 64) {
-      const uint64_t k = grp[t];
-      const int dxy = (int)(k & 3);
-      const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
-      const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
-      const float dyf = (float)((double)py - cy);
-      const float dxf = (float)((double)px - cx);
-      const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
-      long long ti = (long long)rintf(theta);
-      if (ti < 0) ti = 0;
-      // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
-      grp[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
-               ((uint64_t)bx << 1) | ((k >> 3) & 1);
-    }
+    extents_item<256>(b, g, w, s_red);
+  }
+  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (uint32_t it = nlarge + gw; it < total; it += nw) {
+    uint32_t w = 0;
+    work_item(b, cnt, 0, kNumCls, it, &w);
+    extents_item<64>(b, g, w, nullptr);
   }
 }
 

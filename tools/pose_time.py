@@ -16,3 +16,13 @@ for B in (32, 1):
         det.detect_device(d_frames.data_ptr(), frames[0].nbytes, B)
     st, n = det.stage_times()
     print("B=%d" % B, {k: round(v, 4) for k, v in st.items()})
+
+# phase stamps of detection 0 of frame 0 (AT_PHASE_PROBE=1): probe[16 + k]
+if os.environ.get("AT_PHASE_PROBE"):
+    det = rva.GpuDetector(W, H, max_batch=1)
+    for _ in range(3):
+        det.detect_device(d_frames.data_ptr(), frames[0].nbytes, 1)
+    p = det.copy_probe().astype(np.int64)
+    st = p[16:21]
+    print("pose phases (us): polar3 %.2f  OI-1 %.2f  ambiguity %.2f  OI-2 %.2f   steps k1=%d k2=%d" % tuple(
+        list(np.diff(st) / 100.0) + [p[24], p[25]]))
