@@ -1315,7 +1315,7 @@ template <int CAP>
 constexpr int kPeakCap = (CAP / 4 * 4 > 3200 ? CAP / 4 * 4 : 3200) / 8;
 
 template <int NT, int CAP>
-constexpr int kKeySlots = CAP;
+constexpr int kKeySlots = (NT >= 512 && CAP <= 4096) ? 2 * CAP : CAP;  // latency-mode teams: bucket scatter room for CAP keys
 
 template <int NT, int CAP>
 struct BlobShared {

@@ -140,12 +140,15 @@ __device__ M3 polar_rank2_proper(const M3& m) {
   const double a = m.m[0][0] * m.m[0][0] + m.m[1][0] * m.m[1][0] + m.m[2][0] * m.m[2][0];
   const double b = m.m[0][0] * m.m[0][1] + m.m[1][0] * m.m[1][1] + m.m[2][0] * m.m[2][1];
   const double c = m.m[0][1] * m.m[0][1] + m.m[1][1] * m.m[1][1] + m.m[2][1] * m.m[2][1];
-  // sqrt(S) = (S + d I) / tau, d = sqrt(det S), tau = sqrt(tr S + 2d)
-  const double d = sqrt(fmax(a * c - b * b, 0.0));
-  const double tau = sqrt(a + c + 2 * d);
-  // (S + d I)^-1 * tau
+  // sqrt(S) = (S + d I) / tau, d = sqrt(det S), tau = sqrt(tr S + 2d);
+  // det(S + d I) = d tau^2, so (S + d I)^-1 tau = adj(S + d I) / (d tau):
+  // two reciprocal square roots, no square root and no division on the chain
+  const double D = fmax(a * c - b * b, 0.0);
+  const double rd = rsqrt(D);
+  const double d = D * rd;
+  const double rt = rsqrt(a + c + 2 * d);
   const double e00 = a + d, e01 = b, e11 = c + d;
-  const double k = tau / (e00 * e11 - e01 * e01);
+  const double k = rd * rt;
   const double i00 = e11 * k, i01 = -e01 * k, i11 = e00 * k;
   M3 r;
   V3 q0, q1;
