@@ -54,6 +54,8 @@ def parse():
                          "detector stream so the batches in flight run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
+    ap.add_argument("--no-kernel-timer", action="store_true",
+                    help="no HIP events around the dominant kernel (graph replay in the timed region)")
     ap.add_argument("--ingest", choices=["local", "scatter"], default="local",
                     help="local: every rank renders its own frames into its HBM (weak scaling, no data-path "
                          "collective); scatter: frames live on rank 0 and are scattered each step over RCCL "
@@ -251,11 +253,12 @@ def main():
         prof.set_profiling(False)
     dominant = max(stages, key=stages.get) if stages else "k_blob"
     # live per-launch time of the dominant kernel inside the timed region
+    ktimer = None if args.no_kernel_timer else dominant
     for d in dets:
-        d.set_kernel_timer(dominant)
+        d.set_kernel_timer(ktimer)
     run(1)
     for d in dets:
-        d.set_kernel_timer(dominant)  # reset the accumulators
+        d.set_kernel_timer(ktimer)  # reset the accumulators
 
     torch.cuda.synchronize()
     if dist.is_initialized():
@@ -268,7 +271,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kt = [d.kernel_time() for d in dets]
+    kt = [d.kernel_time() for d in dets] if ktimer else [(0.0, 0)]
     k_launches = sum(n for _, n in kt)
     k_ms = sum(ms * n for ms, n in kt) / max(1, k_launches)
     stats = dets[0].batch_stats()

@@ -43,6 +43,8 @@ enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlN
 enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
        kCtlScalars = kCtlNcls + kNumCls };
 
+static constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+
 struct at_detector {
   at_config cfg;
   at_camera cam;
@@ -71,6 +73,11 @@ struct at_detector {
   hipEvent_t ev_done;
   int use_graphs;                         // replay the launch sequence as a hipGraph (AT_NO_GRAPH=1 disables)
   std::map<int, hipGraphExec_t> graphs;   // key: nframes * 4 + fmt
+  // kernel timer under graph replay: the sequence cut around the timed kernel into
+  // three graphs, timing events recorded between them (key: graph key * 32 + stage)
+  struct SplitGraphs { hipGraphExec_t seg[3]; };
+  std::map<int, SplitGraphs> split_graphs;
+  std::vector<hipGraph_t> cap_segs;      // segments collected during one capture
   KernelTimer kt;                         // kt.stage < 0: off
   double kt_ms;
   long long kt_n;
@@ -149,6 +156,9 @@ void at_destroy(at_detector* d) {
   if (d->st2) (void)hipStreamSynchronize(d->st2);
   for (auto& kv : d->graphs) (void)hipGraphExecDestroy(kv.second);
   d->graphs.clear();
+  for (auto& kv : d->split_graphs)
+    for (auto* g : kv.second.seg) (void)hipGraphExecDestroy(g);
+  d->split_graphs.clear();
   for (void* p : d->allocs) (void)hipFree(p);
   if (d->h_ftab) (void)hipHostFree(d->h_ftab);
   if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
@@ -230,7 +240,13 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   d->kt.stage = -1;
-  if (hipEventCreate(&d->kt.t0) != hipSuccess || hipEventCreate(&d->kt.t1) != hipSuccess) return fail(AT_E_HIP);
+  d->kt.split = nullptr;
+  d->kt.ctx = nullptr;
+  // timing-only events: no system-scope fence (cache writeback) when they complete,
+  // so bracketing a kernel does not slow it or its neighbours on other streams
+  if (hipEventCreateWithFlags(&d->kt.t0, kTimingEventFlags) != hipSuccess ||
+      hipEventCreateWithFlags(&d->kt.t1, kTimingEventFlags) != hipSuccess)
+    return fail(AT_E_HIP);
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
   d->nblobwg = std::max(64, ncu * 2);
@@ -408,38 +424,103 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
 // The per-batch sequence: frame table H2D, control block reset, the kernels,
 // control block + detections D2H (all to/from pinned buffers whose addresses
 // never change, so it can be captured once per (nframes, fmt) and replayed).
-static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev) {
+static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev,
+                                  const KernelTimer* kt) {
   hipError_t e;
   if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
   if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
   if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
-                           d->kt.stage >= 0 ? &d->kt : nullptr)))
+                           kt)))
     return e;
   if ((e = hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st))) return e;
   return hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
                         hipMemcpyDeviceToHost, st);
 }
 
+// KernelTimer::split hook while capturing: close the current segment, open the next
+static hipError_t split_capture(void* ctx, int /*which*/) {
+  at_detector* d = (at_detector*)ctx;
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(d->st, &g);
+  if (e != hipSuccess) return e;
+  d->cap_segs.push_back(g);
+  return hipStreamBeginCapture(d->st, hipStreamCaptureModeThreadLocal);
+}
+
+static hipError_t instantiate(hipGraph_t g, hipGraphExec_t* exec) {
+  const hipError_t e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  return e;
+}
+
+// Timed kernel under graph replay (bench roofline): segment before it, the kernel,
+// segment after it, as three graphs with the timing events recorded between them.
+// Not used when the timed kernel sits on the fork branch (its capture spans two
+// streams and cannot be cut there): those launch directly.
+static int enqueue_split(at_detector* d, int nframes, int fmt) {
+  hipStream_t st = d->st;
+  const int key = (nframes * 4 + fmt) * 32 + d->kt.stage;
+  auto it = d->split_graphs.find(key);
+  if (it == d->split_graphs.end()) {
+    d->cap_segs.clear();
+    KernelTimer kt = d->kt;
+    kt.split = split_capture;
+    kt.ctx = d;
+    HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    hipError_t rec = record_sequence(d, nframes, fmt, st, nullptr, &kt);
+    hipGraph_t last = nullptr;
+    const hipError_t end = hipStreamEndCapture(st, &last);
+    if (last) d->cap_segs.push_back(last);
+    if (rec == hipSuccess && end == hipSuccess && d->cap_segs.size() != 3) rec = hipErrorInvalidValue;
+    if (rec != hipSuccess || end != hipSuccess) {
+      for (auto* g : d->cap_segs) (void)hipGraphDestroy(g);
+      d->cap_segs.clear();
+      HIPCHK(rec);
+      HIPCHK(end);
+    }
+    at_detector::SplitGraphs sg{};
+    hipError_t inst = hipSuccess;
+    for (int i = 0; i < 3; i++) {
+      const hipError_t r = instantiate(d->cap_segs[i], &sg.seg[i]);
+      if (r != hipSuccess && inst == hipSuccess) inst = r;
+    }
+    d->cap_segs.clear();
+    if (inst != hipSuccess) {
+      for (auto* g : sg.seg)
+        if (g) (void)hipGraphExecDestroy(g);
+      HIPCHK(inst);
+    }
+    it = d->split_graphs.emplace(key, sg).first;
+  }
+  HIPCHK(hipGraphLaunch(it->second.seg[0], st));
+  HIPCHK(hipEventRecord(d->kt.t0, st));
+  HIPCHK(hipGraphLaunch(it->second.seg[1], st));
+  HIPCHK(hipEventRecord(d->kt.t1, st));
+  HIPCHK(hipGraphLaunch(it->second.seg[2], st));
+  return AT_OK;
+}
+
 static int enqueue(at_detector* d, int nframes, int fmt) {
   hipStream_t st = d->st;
-  // (HIP event-record nodes inside a captured graph do not carry timestamps, so
-  // a timed kernel is launched directly)
-  if (d->profiling || !d->use_graphs || d->kt.stage >= 0) {
-    HIPCHK(record_sequence(d, nframes, fmt, st, d->profiling ? d->ev_stage : nullptr));
+  const bool timed = d->kt.stage >= 0;
+  const bool timed_on_fork = timed && d->st2 && (d->kt.stage == 8 || d->kt.stage == 9);
+  if (d->profiling || !d->use_graphs || timed_on_fork) {
+    HIPCHK(record_sequence(d, nframes, fmt, st, d->profiling ? d->ev_stage : nullptr, timed ? &d->kt : nullptr));
+  } else if (timed) {
+    const int rc = enqueue_split(d, nframes, fmt);
+    if (rc != AT_OK) return rc;
   } else {
     const int key = nframes * 4 + fmt;
     auto it = d->graphs.find(key);
     if (it == d->graphs.end()) {
       hipGraph_t graph = nullptr;
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-      const hipError_t rec = record_sequence(d, nframes, fmt, st, nullptr);
+      const hipError_t rec = record_sequence(d, nframes, fmt, st, nullptr, nullptr);
       const hipError_t end = hipStreamEndCapture(st, &graph);
       HIPCHK(rec);
       HIPCHK(end);
       hipGraphExec_t exec = nullptr;
-      const hipError_t inst = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      HIPCHK(inst);
+      HIPCHK(instantiate(graph, &exec));
       it = d->graphs.emplace(key, exec).first;
     }
     HIPCHK(hipGraphLaunch(it->second, st));
@@ -544,7 +625,7 @@ int at_set_profiling(at_detector* d, int enable) {
   HIPCHK(hipSetDevice(d->device));
   if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));
   if (enable && !d->ev_stage[0])
-    for (int i = 0; i <= kNumStages; i++) HIPCHK(hipEventCreate(&d->ev_stage[i]));
+    for (int i = 0; i <= kNumStages; i++) HIPCHK(hipEventCreateWithFlags(&d->ev_stage[i], kTimingEventFlags));
   d->profiling = enable ? 1 : 0;
   for (int i = 0; i < kNumStages; i++) d->stage_ms[i] = 0;
   d->stage_batches = 0;

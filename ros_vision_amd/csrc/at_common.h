@@ -81,9 +81,15 @@ struct Params {
 constexpr int kProbeWords = 256;
 
 // HIP events bracketing one kernel of the launch sequence (bench roofline).
+// With `split` set (graph replay), the launch sequence calls split(ctx, 0) before
+// and split(ctx, 1) after the timed kernel instead of recording the events, so
+// the caller can cut its stream capture there and record the events between
+// graph segments.
 struct KernelTimer {
   int stage;
   hipEvent_t t0, t1;
+  hipError_t (*split)(void* ctx, int which);
+  void* ctx;
 };
 
 // One detection candidate as produced on the device (before reconcile).

@@ -2490,8 +2490,15 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   auto mark = [&]() {
     if (ev) (void)hipEventRecord(ev[e++], st);
   };
+  hipError_t split_err = hipSuccess;
   auto tk = [&](int stage, hipStream_t s, int which) {
-    if (kt && kt->stage == stage) (void)hipEventRecord(which ? kt->t1 : kt->t0, s);
+    if (!kt || kt->stage != stage) return;
+    if (kt->split) {
+      const hipError_t r = kt->split(kt->ctx, which);
+      if (r != hipSuccess && split_err == hipSuccess) split_err = r;
+    } else {
+      (void)hipEventRecord(which ? kt->t1 : kt->t0, s);
+    }
   };
   mark();
   {
@@ -2577,6 +2584,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
   tk(11, st, 1);
   mark();
+  if (split_err != hipSuccess) return split_err;
   return hipGetLastError();
 }
 
