@@ -24,4 +24,5 @@ def test_reference_fixture_expectations():
     """gpu_detector_test.cu:84-102: id 554 on colorimage, nothing on colorimage_notags."""
     assert [d["id"] for d in VEC["colorimage"]["detections"]] == [554]
     assert VEC["colorimage_notags"]["detections"] == []
+    assert [d["id"] for d in VEC["grayimage"]["detections"]] == [585]
     assert [d["id"] for d in VEC["c1_640x480"]["detections"]] == [0, 1, 2, 554]

@@ -35,6 +35,19 @@ def test_reference_fixture_detects_554(gpu, oracle_mod, golden_dir):
     assert compare_detections(dets, orc.detections()) == []
 
 
+def test_reference_fixture_grayimage_585(gpu, oracle_mod, golden_dir):
+    """Reference fixture test/data/grayimage.jpg -- one tag, id 585."""
+    y = _real(golden_dir, "grayimage")
+    H, W = y.shape
+    det = gpu.GpuDetector(W, H)
+    dets = det.detect(y, gpu.AT_FMT_GRAY8)
+    assert [d.id for d in dets] == [585]
+    orc = oracle_mod.Oracle(W, H)
+    orc.detect(y, 2)
+    assert compare_frame(det, orc) == []
+    assert compare_detections(dets, orc.detections()) == []
+
+
 def test_reference_fixture_no_tags(gpu, oracle_mod, golden_dir):
     """gpu_detector_test.cu:94-102 -- zero detections."""
     y = _real(golden_dir, "colorimage_notags")

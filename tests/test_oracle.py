@@ -23,6 +23,18 @@ def test_colorimage_detects_554(oracle_mod, golden_dir):
     assert np.max(np.abs(d["p"] - expect)) < 3.0
 
 
+def test_grayimage_detects_585(oracle_mod, golden_dir):
+    """Reference fixture test/data/grayimage.jpg: one printed tag captioned id 585."""
+    y = _real(golden_dir, "grayimage")
+    o = oracle_mod.Oracle(y.shape[1], y.shape[0])
+    assert o.detect(y, 2) == 1
+    d = o.detections()[0]
+    assert d["id"] == 585 and d["hamming"] == 0 and d["decision_margin"] > 50
+    # outer black border in the photograph: TL(432,170) TR(772,158) BR(787,504) BL(430,509)
+    expect = np.array([[430, 509], [787, 504], [772, 158], [432, 170]], float)
+    assert np.max(np.abs(d["p"] - expect)) < 3.0
+
+
 def test_colorimage_notags(oracle_mod, golden_dir):
     """gpu_detector_test.cu:94-102: zero detections."""
     y = _real(golden_dir, "colorimage_notags")

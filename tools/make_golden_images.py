@@ -23,7 +23,7 @@ def y_bt601(rgb: np.ndarray) -> np.ndarray:
     return y.astype(np.uint8)
 
 
-for name in ["colorimage", "colorimage_notags"]:
+for name in ["colorimage", "colorimage_notags", "grayimage"]:
     rgb = np.asarray(Image.open(SRC + name + ".jpg").convert("RGB"))
     Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
     print(name, rgb.shape)
