@@ -17,7 +17,8 @@ constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count)
 // k_boundary tiles: 64 x (4 * kBndRows) interior pixels per 256-thread workgroup;
 // each tile owns a fixed region of kBndPts points and kLdsPairSlots pair entries
 constexpr int kBndRows = 4;
-constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel
+constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel (global region per tile)
+constexpr int kBndStage = 1536;                 // of which staged in LDS (1.5 per pixel)
 constexpr int kLdsPairSlots = 512;
 constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)

@@ -546,7 +546,10 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
-  __shared__ uint64_t s_pts[kBndPts];
+  // points staged in LDS up to kBndStage (typical tiles hold ~0.7 points per
+  // pixel); the rare denser tile writes the excess straight to its global
+  // region.  Keeping the stage small keeps 6 workgroups (24 waves) per CU.
+  __shared__ uint64_t s_pts[kBndStage];
   __shared__ uint32_t s_npts, s_nent;
   __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
   __shared__ uint8_t s_tbig[(4 * kBndRows + 1) * 66];
@@ -602,6 +605,8 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __syncthreads();  // LDS tables initialised
   const int x = 1 + blockIdx.x * 64 + threadIdx.x;
   const uint32_t lane = lane_id();
+  const size_t tb = (size_t)f * g.ntb + blockIdx.y * gridDim.x + blockIdx.x;
+  uint64_t* pts_out = b.pts + tb * kBndPts;
   for (int r = 0; r < kBndRows; r++) {
     const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
     const int y = ty0 + ly;
@@ -648,16 +653,19 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
     uint32_t pos = wbase + incl - npk;
 #pragma unroll
     for (int dir = 0; dir < 4; dir++)
-      if (pk[dir]) s_pts[pos++] = pk[dir];
+      if (pk[dir]) {
+        if (pos < (uint32_t)kBndStage) s_pts[pos] = pk[dir];
+        else pts_out[pos] = pk[dir];
+        pos++;
+      }
   }
   __syncthreads();
   // the tile's own regions: points and compacted pair entries, plain stores
   // (no per-frame counter: a device-scope atomic per tile on a per-frame
   // address serialized the tiles of a frame)
   const uint32_t total = s_npts;
-  const size_t tb = (size_t)f * g.ntb + blockIdx.y * gridDim.x + blockIdx.x;
-  uint64_t* pts = b.pts + tb * kBndPts;
-  for (uint32_t i = tid; i < total; i += 256) pts[i] = s_pts[i];
+  const uint32_t staged = total < (uint32_t)kBndStage ? total : (uint32_t)kBndStage;
+  for (uint32_t i = tid; i < staged; i += 256) pts_out[i] = s_pts[i];
   uint64_t* ekey = b.pent_key + tb * kLdsPairSlots;
   uint32_t* ecnt = b.pent_cnt + tb * kLdsPairSlots;
   for (int i = tid; i < kLdsPairSlots; i += 256) {

@@ -221,3 +221,62 @@ def test_pose_disabled_and_camera_to_robot(gpu):
     assert d == sorted(d) and len(tags) == len(on.poses())
     for t in tags:
         assert np.allclose(t.camera, t.robot) and t.camera[2] > 0
+
+
+@pytest.mark.parametrize("kind", ["white_noise", "block_noise_8", "block_noise_24", "checker_10",
+                                  "vstripes_2", "diag_4"])
+def test_noise_frames(gpu, oracle_mod, kind):
+    """Pathological inputs: pixel noise (blob-pair capacity: both sides report it,
+    the reference overflows its 2048-entry extents buffer, apriltag_gpu.cu:129,899)
+    and blocky noise (thousands of rectangles -> many quads and decodes)."""
+    rng = np.random.default_rng({"white_noise": 11, "block_noise_8": 12, "block_noise_24": 13, "checker_10": 14,
+                                 "vstripes_2": 15, "diag_4": 16}[kind])
+    if kind == "white_noise":
+        frame = rng.integers(0, 256, size=(720, 1280), dtype=np.uint8)
+    elif kind == "checker_10":  # > 4096 blob pairs of >= 25 pixels
+        yy, xx = np.mgrid[0:720, 0:1280]
+        frame = np.where(((yy // 10) + (xx // 10)) & 1, 230, 25).astype(np.uint8)
+    elif kind == "vstripes_2":  # ~2 boundary points per pixel: k_boundary tiles overflow their LDS stage
+        yy, xx = np.mgrid[0:720, 0:1280]
+        frame = np.where((xx // 2) & 1, 230, 25).astype(np.uint8)
+    elif kind == "diag_4":
+        yy, xx = np.mgrid[0:720, 0:1280]
+        frame = np.where(((xx + yy) // 4) & 1, 230, 25).astype(np.uint8)
+    else:
+        s = int(kind.rsplit("_", 1)[1])
+        small = rng.integers(0, 256, size=(720 // s + 1, 1280 // s + 1), dtype=np.uint8)
+        frame = np.ascontiguousarray(np.kron(small, np.ones((s, s), np.uint8))[:720, :1280])
+    det = gpu.GpuDetector(1280, 720)
+    dets = det.detect(frame, gpu.AT_FMT_GRAY8)
+    orc = oracle_mod.Oracle(1280, 720)
+    rc = orc.detect(frame, 2)
+    from ros_vision_amd.detector import AT_E_CAPACITY
+    if orc.status() == AT_E_CAPACITY:
+        assert det.frame_status(0) == AT_E_CAPACITY and dets == []
+        return
+    assert rc >= 0 and det.frame_status(0) >= 0
+    assert compare_frame(det, orc) == []
+    assert compare_detections(dets, orc.detections()) == []
+
+
+@pytest.mark.parametrize("dist", [(0.0, 0.0, 0.0, 0.0, 0.0), (0.12, -0.21, 0.004, -0.002, 0.08),
+                                  (-0.3, 0.09, 0.0, 0.0, -0.01)])
+def test_distortion_variants(gpu, oracle_mod, dist):
+    """RefineEdges' UnDistort/ReDistort (apriltag_detect.cu:307-402, incl. the :372
+    p2 term) with other intrinsics and distortion coefficients, k3 != 0 included."""
+    from ros_vision_amd import synth
+    from ros_vision_amd.detector import CameraMatrix, DistCoeffs
+    k1, k2, p1, p2, k3 = dist
+    cam = CameraMatrix(fx=1010.5, cx=655.25, fy=1003.75, cy=371.5)
+    yuyv, gray, truth = synth.stream_frame(1280, 720, 5)
+    det = gpu.GpuDetector(1280, 720, camera_matrix=cam,
+                          distortion_coefficients=DistCoeffs(k1=k1, k2=k2, p1=p1, p2=p2, k3=k3))
+    dets = det.detect(yuyv)
+    prm = oracle_mod.default_params(1280, 720)
+    prm.fx, prm.fy, prm.cx, prm.cy = cam.fx, cam.fy, cam.cx, cam.cy
+    prm.k1, prm.k2, prm.p1, prm.p2, prm.k3 = k1, k2, p1, p2, k3
+    orc = oracle_mod.Oracle(1280, 720, prm)
+    orc.detect(yuyv, 0)
+    assert compare_frame(det, orc) == []
+    assert compare_detections(dets, orc.detections()) == []
+    assert sorted(d.id for d in dets) == sorted(t[0] for t in truth)
