@@ -499,6 +499,19 @@ __device__ uint32_t ht_slot_find(const uint64_t* keys, uint64_t key) {
   return 0xffffffffu;
 }
 
+// Value of lane l-1 in lane l (lane 0: `fill`): one DPP wave_shr:1 move per
+// dword instead of a ds_bpermute round trip through LDS.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) {
+  return (uint64_t)wave_shr1((uint32_t)v, 0) | ((uint64_t)wave_shr1((uint32_t)(v >> 32), 0) << 32);
+}
+// Number of set bits of `mask` below this lane.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 // Length of the run of equal keys starting at this lane (only meaningful for
 // run heads); same_mask bit l means "lane l continues the run of lane l-1".
 __device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
@@ -625,13 +638,15 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
         if (!dedup && v0 + vdl == 255 && s_tbig[edl]) pk[3] = make_qbp(rep0, s_tlab[edl], x, y, 3, vdl > v0);
       }
     }
-    uint32_t npk = 0;
+    uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
 #pragma unroll
     for (int dir = 0; dir < 4; dir++) {
       const bool has = pk[dir] != 0;
-      npk += has;
+      const uint64_t hmask = __ballot(has);
+      below += lanes_below(hmask);
+      wtot += (uint32_t)__popcll(hmask);
       const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
-      const uint64_t prev = __shfl_up(r01, 1);
+      const uint64_t prev = wave_shr1_u64(r01);
       const bool same = has && lane > 0 && prev == r01;
       const uint64_t same_mask = __ballot(same);
       if (has && !same) {
@@ -640,17 +655,10 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       }
     }
     // wave-aggregated append of the points into the LDS staging buffer
-    uint32_t incl = npk;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v = __shfl_up(incl, d);
-      if (lane >= (uint32_t)d) incl += v;
-    }
-    const uint32_t wtot = __shfl(incl, 63);
     uint32_t wbase = 0;
     if (lane == 0 && wtot) wbase = atomicAdd(&s_npts, wtot);
     wbase = __shfl(wbase, 0);
-    uint32_t pos = wbase + incl - npk;
+    uint32_t pos = wbase + below;
 #pragma unroll
     for (int dir = 0; dir < 4; dir++)
       if (pk[dir]) {
@@ -1270,11 +1278,15 @@ __device__ __forceinline__ Mom6 mom_shfl_up(const Mom6& m, int d) {
   return r;
 }
 
+// Blob point sort key (written by k_extents): theta [59:32], dxy [31:30],
+// by [29:20], bx [19:10], b2w [9], W [8:0] (W = (int)(hypotf(gx, gy) + 1) <= 361).
+constexpr int kKeyTheta = 32;
+
 // Compact point word of a sorted blob point: bx [9:0], by [19:10], dxy [21:20],
-// W [30:22] (W = (int)(hypotf(gx, gy) + 1) <= 361).
-__device__ __forceinline__ uint32_t compact_word(uint64_t sk, int32_t Wt) {
-  return (uint32_t)((sk >> 1) & 0x3ff) | ((uint32_t)((sk >> 11) & 0x3ff) << 10) | ((uint32_t)((sk >> 21) & 3) << 20) |
-         ((uint32_t)Wt << 22);
+// W [30:22].
+__device__ __forceinline__ uint32_t compact_word(uint64_t sk) {
+  return (uint32_t)((sk >> 10) & 0x3ff) | ((uint32_t)((sk >> 20) & 0x3ff) << 10) | ((uint32_t)((sk >> 30) & 3) << 20) |
+         ((uint32_t)(sk & 0x1ff) << 22);
 }
 
 // TransformLineFitPoint (apriltag_gpu.cu:631-687) of one compact point word
@@ -1373,7 +1385,7 @@ __device__ bool team_bucket_sort(BlobShared<NT, CAP>& S, int n) {
   const int tid = team_rank<NT>();
   int nb = 32;
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= KEYS/2
-  auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> 23) * (uint64_t)nb) / kThetaSpan); };
+  auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> kKeyTheta) * (uint64_t)nb) / kThetaSpan); };
   uint32_t* bcnt = S.u.bcnt;
   for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
   team_sync<NT>();
@@ -1587,7 +1599,6 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
   const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
-  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
 
   // extents, SelectBlobs and the theta keys come from k_extents
   if (b.pair_sel[(size_t)f * kMaxPairs + rank] == 0) return;  // uniform across the team
@@ -1622,21 +1633,11 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     const uint32_t t = t0 + k;
     if (t < t1) {
       const uint64_t sk = S.keys[t];
-      const int dxy = (int)((sk >> 21) & 3);
-      const int32_t ix2 = (int32_t)(((sk >> 1) & 0x3ff) * 2 + dx_of(dxy)) + 1;
-      const int32_t iy2 = (int32_t)(((sk >> 11) & 0x3ff) * 2 + dy_of(dxy)) + 1;
-      const int32_t ix = ix2 / 2, iy = iy2 / 2;
-      int32_t Wt = 1;
-      if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
-        const int32_t gxv = (int32_t)dec[iy * g.Wd + ix + 1] - (int32_t)dec[iy * g.Wd + ix - 1];
-        const int32_t gyv = (int32_t)dec[(iy + 1) * g.Wd + ix] - (int32_t)dec[(iy - 1) * g.Wd + ix];
-        Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
-      }
-      word[k] = compact_word(sk, Wt);
+      word[k] = compact_word(sk);
       // parity tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
-      const uint64_t pbits = (((sk >> 1) & 0x3ff) << 14) | (((sk >> 11) & 0x3ff) << 4) | ((sk & 1) << 3) |
-                             ((sk >> 21) & 3);
-      if (prm.taps) grp[t] = ((uint64_t)bi << 52) | (((sk >> 23) & 0xfffffff) << 24) | pbits;
+      const uint64_t pbits = (((sk >> 10) & 0x3ff) << 14) | (((sk >> 20) & 0x3ff) << 4) | (((sk >> 9) & 1) << 3) |
+                             ((sk >> 30) & 3);
+      if (prm.taps) grp[t] = ((uint64_t)bi << 52) | (((sk >> kKeyTheta) & 0xfffffff) << 24) | pbits;
       mom_add(csum, point_mom(word[k]));
     }
   }
@@ -1943,19 +1944,35 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   const uint32_t rank = w & 0xffff;
   const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
+  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
   uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
   int32_t sgx = 0, sgy = 0;
   int64_t spg = 0;
-  for (uint32_t t = tid; t < n; t += NT) {
-    const uint64_t k = grp[t];
-    const int dxy = (int)(k & 3);
-    const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
-    const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
-    const bool b2w = (k & 8) != 0;
-    const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
-    mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
-    sgx += gx; sgy += gy;
-    spg += (int64_t)px * gx + (int64_t)py * gy;
+  // U points per lane per round, every load of a round issued before any is
+  // used; the first round's keys stay in registers for the key pass below
+  constexpr int U = 8;
+  uint64_t kr[U];
+  for (uint32_t base = 0; base < n; base += NT * U) {
+    uint64_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = base + u * NT + tid;
+      kk[u] = t < n ? grp[t] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (base == 0) kr[u] = kk[u];
+      if (base + u * NT + tid >= n) continue;
+      const uint64_t k = kk[u];
+      const int dxy = (int)(k & 3);
+      const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
+      const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
+      const bool b2w = (k & 8) != 0;
+      const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
+      mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
+      sgx += gx; sgy += gy;
+      spg += (int64_t)px * gx + (int64_t)py * gy;
+    }
   }
   mnx = wave_reduce(mnx, MinOp()); mxx = wave_reduce(mxx, MaxOp());
   mny = wave_reduce(mny, MinOp()); mxy = wave_reduce(mxy, MaxOp());
@@ -1987,19 +2004,53 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   if (!keep) return;  // uniform across the team
   if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
   const double cx = ext_cx(e), cy = ext_cy(e);
-  for (uint32_t t = tid; t < n; t += NT) {
-    const uint64_t k = grp[t];
-    const int dxy = (int)(k & 3);
-    const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
-    const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
-    const float dyf = (float)((double)py - cy);
-    const float dxf = (float)((double)px - cx);
-    const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
-    long long ti = (long long)rintf(theta);
-    if (ti < 0) ti = 0;
-    // order (theta, plane, y, x) == P6 stable order; b2w rides in bit 0 (never decides)
-    grp[t] = ((uint64_t)(ti & 0xfffffff) << 23) | ((uint64_t)dxy << 21) | ((uint64_t)by << 11) |
-             ((uint64_t)bx << 1) | ((k >> 3) & 1);
+  for (uint32_t base = 0; base < n; base += NT * U) {
+    uint64_t kk[U];
+    uint32_t gp[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = base + u * NT + tid;
+      kk[u] = base == 0 ? kr[u] : (t < n ? grp[t] : 0);
+    }
+    // line-fit weight of TransformLineFitPoint (apriltag_gpu.cu:631-687): gradient
+    // of the decimated image at ((px + 1) / 2, (py + 1) / 2); the four bytes of
+    // every point of the round are loaded first (out-of-range: a fixed pixel)
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t k = kk[u];
+      const int dxy = (int)(k & 3);
+      const int32_t ix = (int32_t)(((k >> 14) & 0x3ff) * 2 + dx_of(dxy) + 1) / 2;
+      const int32_t iy = (int32_t)(((k >> 4) & 0x3ff) * 2 + dy_of(dxy) + 1) / 2;
+      const bool in = base + u * NT + tid < n && ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd;
+      const int32_t at = in ? iy * g.Wd + ix : g.Wd + 1;
+      gp[u] = (uint32_t)dec[at - 1] | ((uint32_t)dec[at + 1] << 8) | ((uint32_t)dec[at - g.Wd] << 16) |
+              ((uint32_t)dec[at + g.Wd] << 24);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = base + u * NT + tid;
+      if (t >= n) continue;
+      const uint64_t k = kk[u];
+      const int dxy = (int)(k & 3);
+      const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
+      const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
+      const float dyf = (float)((double)py - cy);
+      const float dxf = (float)((double)px - cx);
+      const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
+      long long ti = (long long)rintf(theta);
+      if (ti < 0) ti = 0;
+      const int32_t ix = (int32_t)(px + 1) / 2, iy = (int32_t)(py + 1) / 2;
+      int32_t Wt = 1;
+      if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
+        const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
+        const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
+        Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+      }
+      // sort key: order (theta, plane, y, x) == P6 stable order; b2w and W ride in
+      // the low bits (never decide: (plane, y, x) is unique)
+      grp[t] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
+               ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
+    }
   }
 }
 
