@@ -17,6 +17,7 @@
 // All float arithmetic is compiled with -ffp-contract=off and uses at_detmath.h
 // for transcendental functions so that results are bit-identical to the CPU
 // oracle (oracle/ao_oracle.c).
+#include <limits>
 #include <hip/hip_runtime.h>
 
 #include <float.h>
@@ -42,17 +43,66 @@ __device__ __forceinline__ uint64_t mix_hash(uint64_t k) {
 __device__ __forceinline__ int dx_of(int dxy) { return dxy == 3 ? -1 : (dxy == 2 ? 0 : 1); }
 __device__ __forceinline__ int dy_of(int dxy) { return dxy == 0 ? 0 : 1; }
 
+// ---- wave64 primitives on DPP (GFX9 row_shr / row_bcast): one VALU move per
+// dword and step instead of an LDS ds_bpermute / ds_swizzle round trip --------
+template <int CTRL, int ROW_MASK, typename T>
+__device__ __forceinline__ T dpp_move(T v, T old) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "dpp_move: 32- or 64-bit values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                             CTRL, ROW_MASK, 0xf, false));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v), o = __builtin_bit_cast(uint64_t, old);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)u, CTRL, ROW_MASK, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(u >> 32), CTRL,
+                                                              ROW_MASK, 0xf, false);
+    return __builtin_bit_cast(T, (uint64_t)lo | ((uint64_t)hi << 32));
+  }
+}
+
+// inclusive wave scan: lanes whose DPP source is out of range combine `id`
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T x, Op op, T id) {
+  x = op(x, dpp_move<0x111, 0xf>(x, id));  // row_shr:1
+  x = op(x, dpp_move<0x112, 0xf>(x, id));  // row_shr:2
+  x = op(x, dpp_move<0x114, 0xf>(x, id));  // row_shr:4
+  x = op(x, dpp_move<0x118, 0xf>(x, id));  // row_shr:8
+  x = op(x, dpp_move<0x142, 0xa>(x, id));  // row_bcast:15 -> rows 1, 3
+  x = op(x, dpp_move<0x143, 0xc>(x, id));  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// value of lane `l` in every lane (scalar read)
+template <typename T>
+__device__ __forceinline__ T wave_read(T v, int l) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  } else {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(T, (uint64_t)lo | ((uint64_t)hi << 32));
+  }
+}
+
+struct MinOp {
+  template <typename T> __device__ T operator()(T a, T c) const { return a < c ? a : c; }
+  template <typename T> __device__ static T identity() { return std::numeric_limits<T>::max(); }
+};
+struct MaxOp {
+  template <typename T> __device__ T operator()(T a, T c) const { return a > c ? a : c; }
+  template <typename T> __device__ static T identity() { return std::numeric_limits<T>::lowest(); }
+};
+struct AddOp {
+  template <typename T> __device__ T operator()(T a, T c) const { return a + c; }
+  template <typename T> __device__ static T identity() { return T(0); }
+};
+
 // ---- block reductions (256 threads = 4 waves) ------------------------------
 template <typename T, typename Op>
 __device__ T wave_reduce(T v, Op op) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v = op(v, __shfl_xor(v, d));
-  return v;
+  return wave_read(wave_incl_scan(v, op, Op::template identity<T>()), 63);
 }
-
-struct MinOp { template <typename T> __device__ T operator()(T a, T c) const { return a < c ? a : c; } };
-struct MaxOp { template <typename T> __device__ T operator()(T a, T c) const { return a > c ? a : c; } };
-struct AddOp { template <typename T> __device__ T operator()(T a, T c) const { return a + c; } };
 
 template <typename T, typename Op>
 __device__ T block_reduce(T v, Op op, T* s_tmp /* >= NW */, int NW) {
@@ -71,11 +121,7 @@ __device__ T block_reduce(T v, Op op, T* s_tmp /* >= NW */, int NW) {
 template <typename T>
 __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
   const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T u = __shfl_up(v, d);
-    if (lane >= (uint32_t)d) v = v + u;
-  }
+  v = wave_incl_scan(v, AddOp(), T(0));
   const int w = threadIdx.x >> 6;
   __syncthreads();
   if (lane == 63) s_tmp[w] = v;
@@ -851,13 +897,8 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const int i0 = tid * 4;
   const uint32_t c0 = s_cnt[i0], c1 = s_cnt[i0 + 1], c2 = s_cnt[i0 + 2], c3 = s_cnt[i0 + 3];
   const uint32_t tsum = c0 + c1 + c2 + c3;
-  uint32_t incl = tsum;
+  const uint32_t incl = wave_incl_scan(tsum, AddOp(), 0u);
   const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d);
-    if (lane >= (uint32_t)d) incl += v;
-  }
   if (lane == 63) s_wsum[tid >> 6] = incl;
   __syncthreads();
   uint32_t wbase = 0;
@@ -1052,13 +1093,8 @@ __device__ T team_reduce(T v, Op op, T* s_tmp) {
 template <int NT, typename T>
 __device__ T team_incl_scan(T v, T* s_tmp, T* total) {
   if constexpr (NT == 64) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const T u = __shfl_up(v, d);
-      if (lane >= (uint32_t)d) v = v + u;
-    }
-    *total = __shfl(v, 63);
+    v = wave_incl_scan(v, AddOp(), T(0));
+    *total = wave_read(v, 63);
     return v;
   } else {
     return block_incl_scan(v, s_tmp, total, NT / 64);
@@ -1528,12 +1564,13 @@ __device__ __forceinline__ void team_extents(BlobShared<NT, CAP>& S, uint32_t& m
 template <int NT, int CAP>
 __device__ __forceinline__ Mom6 team_excl_scan_mom(BlobShared<NT, CAP>& S, const Mom6& v, Mom6* total) {
   const uint32_t lane = lane_id();
-  Mom6 incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const Mom6 u = mom_shfl_up(incl, d);
-    if (lane >= (uint32_t)d) mom_add(incl, u);
-  }
+  Mom6 incl;
+  incl.Mx = wave_incl_scan(v.Mx, AddOp(), 0u);
+  incl.My = wave_incl_scan(v.My, AddOp(), 0u);
+  incl.W = wave_incl_scan(v.W, AddOp(), 0u);
+  incl.Mxx = wave_incl_scan(v.Mxx, AddOp(), (uint64_t)0);
+  incl.Myy = wave_incl_scan(v.Myy, AddOp(), (uint64_t)0);
+  incl.Mxy = wave_incl_scan(v.Mxy, AddOp(), (uint64_t)0);
   Mom6 ex = incl;
   mom_sub(ex, v);
   if constexpr (NT > 64) {
@@ -1548,7 +1585,8 @@ __device__ __forceinline__ Mom6 team_excl_scan_mom(BlobShared<NT, CAP>& S, const
     }
     *total = tot;
   } else {
-    *total = mom_shfl(incl, 63);
+    *total = Mom6{wave_read(incl.Mx, 63), wave_read(incl.My, 63), wave_read(incl.W, 63),
+                  wave_read(incl.Mxx, 63), wave_read(incl.Myy, 63), wave_read(incl.Mxy, 63)};
   }
   return ex;
 }
