@@ -79,8 +79,12 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_extents":  # candidate points read (bounded by all boundary points), kept points' keys written
         return 8 * stats.get("boundary_points", 0) + 8 * (stats.get("small_blob_points", 0) +
                                                           stats.get("large_blob_points", 0))
-    if kernel in ("k_thr_ccl", "k_ccl_final"):
-        return nf * 9 * Wd * Hd                            # dec/thr in, labels/sizes out
+    if kernel == "k_thr_ccl":
+        return nf * 9 * Wd * Hd                            # dec in; thr, parents, sizes out
+    if kernel == "k_ccl_border":  # per 32x32 tile: 47 border blocks, thr bytes + parent words
+        return nf * ((Wd + 31) // 32) * ((Hd + 31) // 32) * 47 * 16
+    if kernel == "k_pose":  # per candidate detection: H + corners in, R, t, errors out
+        return stats.get("candidates", 0) * (72 + 64 + 112)
     return None
 
 
