@@ -2564,14 +2564,27 @@ hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
 // K11: tag pose of every decoded candidate (row A23: estimate_tag_pose at
 // apriltags_cuda_detector.cu:433), one thread per detection.
 // ---------------------------------------------------------------------------
+// One detection per quad of lanes (16 per wave): the four lanes compute the
+// same pose, splitting only the quartic's root brackets; lane 0 of the quad stores.
+constexpr int kPoseLanes = 4;
 __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
   const int f = blockIdx.y;
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t i = blockIdx.x * (64 / kPoseLanes) + threadIdx.x / kPoseLanes;
+  const int sub = (int)(threadIdx.x % kPoseLanes);
   const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
-  if (i >= n) return;
+  if (i >= n) return;  // uniform across the quad
   DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
-  pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, d.pose_R, d.pose_t, d.pose_err,
-                          (prm.probe && f == 0 && i == 0) ? b.probe + 16 : nullptr);
+  double R[9], t[3], err[2];
+  pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
+                          (prm.probe && f == 0 && i == 0 && sub == 0) ? b.probe + 16 : nullptr);
+  if (sub == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) d.pose_R[k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) d.pose_t[k] = t[k];
+    d.pose_err[0] = err[0];
+    d.pose_err[1] = err[1];
+  }
 }
 
 // st2/fork/join: a second stream on which the small-blob kernel runs beside
@@ -2678,7 +2691,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(10, st, 1);
   mark();
   tk(11, st, 0);
-  if (prm.tag_size > 0) hipLaunchKernelGGL(k_pose, dim3((kMaxDets + 63) / 64, B), dim3(64), 0, st, b, prm);
+  if (prm.tag_size > 0)
+    hipLaunchKernelGGL(k_pose, dim3((kMaxDets * kPoseLanes + 63) / 64, B), dim3(64), 0, st, b, prm);
   tk(11, st, 1);
   mark();
   if (split_err != hipSuccess) return split_err;

@@ -14,8 +14,8 @@
 //     column (tag corners lie in z = 0), so U V' restricted to the first two
 //     columns is the polar factor of the 3x2 block A (A'A)^-1/2 (2x2 closed
 //     form), and the det(R) < 0 column-2 flip leaves column 2 = c0 x c1.
-// One thread per detection; everything in double.  The k_pose chain is
-// latency-bound (one wave per 64 tags), so FMA contraction is allowed here
+// Four lanes per detection (the quartic's root brackets in parallel); everything
+// in double.  The k_pose chain is latency-bound, so FMA contraction is allowed here
 // (float tolerance 1e-4, unlike the bit-exact integer stages) and the
 // per-step sums are balanced trees.
 #pragma once
@@ -311,12 +311,32 @@ __device__ __forceinline__ double polyval(const double* p, int degree, double x)
   return ret;
 }
 
-// solve_poly_approx for degree <= 4, unrolled over degrees 1..4 (no recursion)
+// Four lanes (a DPP quad) work on one detection: every quantity is computed
+// redundantly on all four, except the root brackets of solve_poly_approx, which
+// are independent and are solved one per lane; the roots are then gathered in
+// bracket order by quad broadcasts, so each lane ends up with exactly the
+// sequential result.
+template <int J>
+__device__ __forceinline__ double quad_bcast(double v) {
+  constexpr int kCtrl = J | (J << 2) | (J << 4) | (J << 6);  // quad_perm:[J,J,J,J]
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, kCtrl, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), kCtrl, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+template <int J>
+__device__ __forceinline__ int quad_bcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, J | (J << 2) | (J << 4) | (J << 6), 0xf, 0xf, false);
+}
+
+// solve_poly_approx for degree <= 4, unrolled over degrees 1..4 (no recursion).
 // The outer brackets [-1000, r_1] and [r_n, 1000] are shrunk to the Cauchy
 // bound 1 + max|p_i / p_deg| when it is smaller: no real root lies beyond it
 // (nor, by Gauss-Lucas, a derivative root), so the sign test and the bracketed
 // root are unchanged while the safeguarded Newton needs far fewer steps.
-__device__ int solve_poly_level(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
+// Bracket `sub` (<= n_der <= 3) is this lane's; the caller's quad supplies the rest.
+__device__ int solve_poly_level(const double* p, int degree, const double* der_roots, int n_der, double* roots,
+                                int sub) {
   double MAX_ROOT = 1000;
   if (p[degree] != 0) {
     double cb = 0;
@@ -325,8 +345,10 @@ __device__ int solve_poly_level(const double* p, int degree, const double* der_r
   }
   double p_der[4];
   for (int i = 0; i < degree; i++) p_der[i] = (i + 1) * p[i + 1];
-  int n = 0;
-  for (int i = 0; i <= n_der; i++) {
+  double my_root = 0;
+  int my_has = 0;
+  if (sub <= n_der) {
+    const int i = sub;
     const double mn = i == 0 ? -MAX_ROOT : der_roots[i - 1];
     const double mx = i == n_der ? MAX_ROOT : der_roots[i];
     const double fmn = polyval(p, degree, mn), fmx = polyval(p, degree, mx);
@@ -358,15 +380,27 @@ __device__ int solve_poly_level(const double* p, int degree, const double* der_r
         if (f > 0) upper = root;
         else lower = root;
       }
-      roots[n++] = root;
+      my_root = root;
+      my_has = 1;
     } else if (fmx == 0) {
-      roots[n++] = mx;
+      my_root = mx;
+      my_has = 1;
     }
   }
+  int n = 0;
+  double r;
+  r = quad_bcast<0>(my_root);
+  if (quad_bcast<0>(my_has)) roots[n++] = r;
+  r = quad_bcast<1>(my_root);
+  if (quad_bcast<1>(my_has)) roots[n++] = r;
+  r = quad_bcast<2>(my_root);
+  if (quad_bcast<2>(my_has)) roots[n++] = r;
+  r = quad_bcast<3>(my_root);
+  if (quad_bcast<3>(my_has)) roots[n++] = r;
   return n;
 }
 
-__device__ int solve_quartic_approx(const double* p4, double* roots) {
+__device__ int solve_quartic_approx(const double* p4, double* roots, int sub) {
   // derivative chain: p4 (deg 4) -> p3 -> p2 -> p1 (linear)
   double d3[4], d2[3], d1[2];
   for (int i = 0; i < 4; i++) d3[i] = (i + 1) * p4[i + 1];
@@ -378,12 +412,12 @@ __device__ int solve_quartic_approx(const double* p4, double* roots) {
     r1[0] = -d1[0] / d1[1];
     n1 = 1;
   }
-  const int n2 = solve_poly_level(d2, 2, r1, n1, r2);
-  const int n3 = solve_poly_level(d3, 3, r2, n2, r3);
-  return solve_poly_level(p4, 4, r3, n3, roots);
+  const int n2 = solve_poly_level(d2, 2, r1, n1, r2, sub);
+  const int n3 = solve_poly_level(d3, 3, r2, n2, r3, sub);
+  return solve_poly_level(p4, 4, r3, n3, roots, sub);
 }
 
-__device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, const M3& R, M3* out) {
+__device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, const M3& R, M3* out, int sub) {
   const V3 R_t_3 = v_scale(t, 1.0 / sqrt(v_dot(t, t)));
   const V3 e_x = {{1, 0, 0}};
   V3 R_t_1 = v_sub(e_x, v_scale(R_t_3, v_dot(e_x, R_t_3)));
@@ -463,7 +497,7 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
   }
   const double poly[5] = {a1, 2 * a2 - 4 * a0, 3 * a3 - 3 * a1, 4 * a4 - 2 * a2, -a3};
   double roots[4];
-  const int n_roots = solve_quartic_approx(poly, roots);
+  const int n_roots = solve_quartic_approx(poly, roots, sub);
   double minimum = 0;
   int n_minima = 0;
   for (int i = 0; i < n_roots; i++) {
@@ -489,8 +523,10 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
 }
 
 // estimate_tag_pose: writes R (row-major), t and the winning error.
+// sub: this lane's index in the detection's quad (see solve_poly_level); all
+// four lanes return the same pose.
 __device__ void estimate_tag_pose(const double H[9], const double corners[4][2], double fx, double fy, double cx,
-                                  double cy, double tagsize, double* R_out, double* t_out, double* err_out,
+                                  double cy, double tagsize, double* R_out, double* t_out, double* err_out, int sub,
                                   uint64_t* stamps = nullptr) {
   if (stamps) stamps[0] = wall_clock64();
   const double s = tagsize / 2.0;
@@ -531,7 +567,7 @@ __device__ void estimate_tag_pose(const double H[9], const double corners[4][2],
   M3 R2;
   V3 t2 = {{0, 0, 0}};
   double err2 = HUGE_VAL;
-  const bool amb = fix_pose_ambiguities(v, p, t1, R1, &R2);
+  const bool amb = fix_pose_ambiguities(v, p, t1, R1, &R2, sub);
   if (stamps) stamps[3] = wall_clock64();
   if (amb) err2 = orthogonal_iteration(v, p, &t2, &R2, 50, &k2);
   if (stamps) {
