@@ -72,6 +72,11 @@ __device__ __forceinline__ T wave_incl_scan(T x, Op op, T id) {
   return x;
 }
 
+// value of lane + 1 (lane 63: 0): DPP wave_shl:1
+__device__ __forceinline__ uint32_t wave_read_next(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+
 // value of lane `l` in every lane (scalar read)
 template <typename T>
 __device__ __forceinline__ T wave_read(T v, int l) {
@@ -1403,7 +1408,7 @@ struct BlobShared {
   int32_t pi[16];
   double lines[4][4];
   uint32_t pacc[21];  // probe accumulators + processed-point count of this team
-  uint64_t t_last;
+  uint64_t t_last, t_item;
 };
 
 // Sort of a blob's (theta, plane, y, x) keys: theta is near-uniform around the
@@ -1591,6 +1596,113 @@ __device__ __forceinline__ Mom6 team_excl_scan_mom(BlobShared<NT, CAP>& S, const
   return ex;
 }
 
+// Wave-team sort (NT == 64, 64 <= n <= CAP <= 512 keys): the keys stay in
+// registers (CAP / 64 per lane) through a counting sort by theta bucket (LDS
+// histogram, scan, scatter with LDS atomics) and an in-bucket rank, so no second
+// LDS key array is needed and blobs up to CAP points take this path.  Buckets
+// are theta >> s (nb = 2^m buckets of width 2^(26-m); theta < 2^26).  Returns
+// false with the keys in S.keys in load order when a bucket exceeds 32 keys.
+template <int CAP>
+__device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, int n) {
+  static_assert(CAP % 64 == 0 && CAP <= 512, "wave sort: at most 8 keys per lane");
+  static_assert(kThetaSpan <= (1ull << 26), "theta fits 26 bits");
+  constexpr int KPL = CAP / 64;
+  const uint32_t lane = lane_id();
+  uint64_t kv[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    const int t = j * 64 + (int)lane;
+    kv[j] = t < n ? grp[t] : ~0ull;
+  }
+  int nb = 32;
+  while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n, power of two, <= 256
+  const int sh = 26 - __builtin_ctz((unsigned)nb);
+  auto bucket = [&](uint64_t k) { return (uint32_t)((k >> kKeyTheta) >> sh); };
+  uint32_t* bcnt = S.u.bcnt;  // two u16 counters per word
+  for (int i = (int)lane; i < nb / 2; i += 64) bcnt[i] = 0;
+  team_sync<64>();
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    if (j * 64 + (int)lane < n) {
+      const uint32_t bk = bucket(kv[j]);
+      atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+    }
+  }
+  team_sync<64>();
+  // exclusive scan of the nb counts, each lane owning nb/64 (or one) consecutive buckets
+  const int per = nb >= 64 ? nb / 64 : 1;
+  const int b0 = (int)lane * per;
+  uint32_t cval[4], loc = 0, mx = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    cval[j] = 0;
+    if (j < per && b0 + j < nb) {
+      const uint32_t bb = (uint32_t)(b0 + j);
+      cval[j] = (bcnt[bb >> 1] >> ((bb & 1) * 16)) & 0xffffu;
+      loc += cval[j];
+      mx = cval[j] > mx ? cval[j] : mx;
+    }
+  }
+  const uint32_t incl = wave_incl_scan(loc, AddOp(), 0u);
+  mx = wave_reduce(mx, MaxOp());
+  if (mx > 32) {  // uniform: fall back to the bitonic sort on S.keys
+#pragma unroll
+    for (int j = 0; j < KPL; j++) {
+      const int t = j * 64 + (int)lane;
+      if (t < n) S.keys[t] = kv[j];
+    }
+    team_sync<64>();
+    return false;
+  }
+  team_sync<64>();
+  // bucket starts in place (u16 each)
+  uint32_t run = incl - loc;
+  uint32_t st[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    st[j] = run;
+    if (j < per && b0 + j < nb) run += cval[j];
+  }
+  if (per >= 2) {
+#pragma unroll
+    for (int j = 0; j < 4; j += 2)
+      if (j < per) bcnt[(b0 + j) >> 1] = st[j] | (st[j + 1] << 16);
+  } else if (b0 < nb) {  // one bucket per lane: the even lane writes both halves of the word
+    const uint32_t other = wave_read_next(st[0]);
+    if ((b0 & 1) == 0) bcnt[b0 >> 1] = st[0] | (other << 16);
+  }
+  team_sync<64>();
+  // scatter: after it each bucket's counter holds its end
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    if (j * 64 + (int)lane < n) {
+      const uint32_t bk = bucket(kv[j]);
+      const uint32_t old = atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+      S.keys[(old >> ((bk & 1) * 16)) & 0xffffu] = kv[j];
+    }
+  }
+  team_sync<64>();
+  uint32_t rk[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    rk[j] = 0;
+    if (j * 64 + (int)lane < n) {
+      const uint32_t bk = bucket(kv[j]);
+      const uint32_t hi = (bcnt[bk >> 1] >> ((bk & 1) * 16)) & 0xffffu;
+      const uint32_t lo = bk ? (bcnt[(bk - 1) >> 1] >> (((bk - 1) & 1) * 16)) & 0xffffu : 0u;
+      uint32_t r = lo;
+      for (uint32_t i = lo; i < hi; i++) r += S.keys[i] < kv[j];
+      rk[j] = r;
+    }
+  }
+  team_sync<64>();
+#pragma unroll
+  for (int j = 0; j < KPL; j++)
+    if (j * 64 + (int)lane < n) S.keys[rk[j]] = kv[j];
+  team_sync<64>();
+  return true;
+}
+
 // Inclusive prefix moments P(i) of the blob's points: the owning chunk's base
 // plus the chunk's words up to i.  Called by every lane of the team (the base
 // of a wave-sized team comes by lane shuffle); inactive lanes get zero.
@@ -1623,7 +1735,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   const uint32_t lane = lane_id();
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k]);
   // the accumulators live in the team's LDS, not in registers
-  if (prm.probe && tid == 0) S.t_last = wall_clock64();
+  if (prm.probe && tid == 0) S.t_last = S.t_item = wall_clock64();
   auto phase = [&](int k) {  // accumulated per team, flushed once per kernel
     if (prm.probe && tid == 0) {
       const uint64_t now = wall_clock64();
@@ -1643,10 +1755,20 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
   const uint32_t bi = rank & 0xfff;
   phase(0);
-  for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
-  phase(1);
-  team_sync<NT>();
-  if (!team_bucket_sort<NT, CAP>(S, (int)n)) {
+  bool sorted = false;
+  if constexpr (NT == 64) {
+    if (n >= 64) {  // keys go straight from global memory into registers
+      phase(1);
+      sorted = wave_bucket_sort<CAP>(S, grp, (int)n);
+    }
+  }
+  if (!sorted && (NT != 64 || n < 64)) {
+    for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
+    phase(1);
+    team_sync<NT>();
+    sorted = team_bucket_sort<NT, CAP>(S, (int)n);
+  }
+  if (!sorted) {
     int np2 = 64;
     while (np2 < (int)n) np2 <<= 1;
     for (int t = (int)n + tid; t < np2; t += NT) S.keys[t] = ~0ull;
@@ -1945,6 +2067,9 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     }
   }
   phase(9);
+  if (prm.probe && tid == 0)  // slowest item of the kernel: (wall-clock ticks << 20) | points
+    atomicMax((unsigned long long*)&b.probe[NT == 64 ? 200 : 201],
+              (unsigned long long)(((S.t_last - S.t_item) << 20) | n));
   team_sync<NT>();
 }
 

@@ -34,3 +34,7 @@ for kind, base in (("small", 64), ("large", 80), ("decode", 128)):
         if p[base + k] or p[base + 32 + k]:
             print("  phase %d %-16s total %9.1f us  count %6d  mean %7.2f us" % (
                 k, names.get(k, ""), p[base + k] / 100.0, p[base + 32 + k], p[base + k] / 100.0 / max(1, p[base + 32 + k])))
+
+for name, idx in (("small", 200), ("large", 201)):
+    v = int(det.copy_probe().astype(np.int64)[idx])
+    print("slowest %s item: %.2f us, %d points" % (name, (v >> 20) / 100.0, v & 0xfffff))
