@@ -1596,6 +1596,11 @@ __device__ __forceinline__ Mom6 team_excl_scan_mom(BlobShared<NT, CAP>& S, const
   return ex;
 }
 
+// largest theta bucket ranked in place: a rank costs one LDS read per bucket
+// key, still well below a bitonic sort (log2(n)^2 / 2 passes) for crowded
+// buckets (long straight borders seen from the blob centre)
+constexpr uint32_t kRegSortMaxBucket = 512;
+
 // Wave-team sort (NT == 64, 64 <= n <= CAP <= 512 keys): the keys stay in
 // registers (CAP / 64 per lane) through a counting sort by theta bucket (LDS
 // histogram, scan, scatter with LDS atomics) and an in-bucket rank, so no second
@@ -1645,7 +1650,7 @@ __device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, in
   }
   const uint32_t incl = wave_incl_scan(loc, AddOp(), 0u);
   mx = wave_reduce(mx, MaxOp());
-  if (mx > 32) {  // uniform: fall back to the bitonic sort on S.keys
+  if (mx > kRegSortMaxBucket) {  // uniform: fall back to the bitonic sort on S.keys
 #pragma unroll
     for (int j = 0; j < KPL; j++) {
       const int t = j * 64 + (int)lane;
@@ -1703,6 +1708,111 @@ __device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, in
   return true;
 }
 
+// Workgroup-team variant of wave_bucket_sort for the blobs whose keys do not
+// fit twice in S.keys (n > KEYS / 2): the keys stay in registers (CAP / NT per
+// thread) through the counting sort and the in-bucket rank, instead of falling
+// back to a bitonic sort of the next power of two.
+template <int NT, int CAP>
+__device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp, int n) {
+  static_assert(NT > 64 && CAP % NT == 0, "workgroup teams");
+  constexpr int KPL = CAP / NT;
+  constexpr int KEYS = kKeySlots<NT, CAP>;
+  static_assert(KPL <= 16, "at most 16 keys per thread");
+  const int tid = team_rank<NT>();
+  uint64_t kv[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    const int t = j * NT + tid;
+    kv[j] = t < n ? grp[t] : ~0ull;
+  }
+  int nb = 32;
+  while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n, power of two
+  if (nb / 2 > KEYS / 4) return false;
+  const int sh = 26 - __builtin_ctz((unsigned)nb);
+  auto bucket = [&](uint64_t k) { return (uint32_t)((k >> kKeyTheta) >> sh); };
+  uint32_t* bcnt = S.u.bcnt;
+  for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
+  team_sync<NT>();
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    if (j * NT + tid < n) {
+      const uint32_t bk = bucket(kv[j]);
+      atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+    }
+  }
+  team_sync<NT>();
+  const int per = nb >= NT ? nb / NT : 1;  // <= 8 (nb <= 2048 for 256 threads)
+  const int b0 = tid * per;
+  uint32_t cval[8], loc = 0, mx = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    cval[j] = 0;
+    if (j < per && b0 + j < nb) {
+      const uint32_t bb = (uint32_t)(b0 + j);
+      cval[j] = (bcnt[bb >> 1] >> ((bb & 1) * 16)) & 0xffffu;
+      loc += cval[j];
+      mx = cval[j] > mx ? cval[j] : mx;
+    }
+  }
+  uint32_t tot;
+  const uint32_t incl = team_incl_scan<NT>(loc, S.red_u32, &tot);
+  mx = team_reduce<NT>(mx, MaxOp(), S.red_u32);
+  if (mx > kRegSortMaxBucket) {  // uniform: keys back to S.keys for the bitonic fallback
+#pragma unroll
+    for (int j = 0; j < KPL; j++) {
+      const int t = j * NT + tid;
+      if (t < n) S.keys[t] = kv[j];
+    }
+    team_sync<NT>();
+    return false;
+  }
+  team_sync<NT>();
+  uint32_t run = incl - loc;
+  uint32_t st[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    st[j] = run;
+    if (j < per && b0 + j < nb) run += cval[j];
+  }
+  if (per >= 2) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2)
+      if (j < per) bcnt[(b0 + j) >> 1] = st[j] | (st[j + 1] << 16);
+  } else if (b0 < nb) {
+    const uint32_t other = wave_read_next(st[0]);  // neighbours share a word (same wave: NT >= nb's lane pairs)
+    if ((b0 & 1) == 0) bcnt[b0 >> 1] = st[0] | (other << 16);
+  }
+  team_sync<NT>();
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    if (j * NT + tid < n) {
+      const uint32_t bk = bucket(kv[j]);
+      const uint32_t old = atomicAdd(&bcnt[bk >> 1], 1u << ((bk & 1) * 16));
+      S.keys[(old >> ((bk & 1) * 16)) & 0xffffu] = kv[j];
+    }
+  }
+  team_sync<NT>();
+  uint32_t rk[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    rk[j] = 0;
+    if (j * NT + tid < n) {
+      const uint32_t bk = bucket(kv[j]);
+      const uint32_t hi = (bcnt[bk >> 1] >> ((bk & 1) * 16)) & 0xffffu;
+      const uint32_t lo = bk ? (bcnt[(bk - 1) >> 1] >> (((bk - 1) & 1) * 16)) & 0xffffu : 0u;
+      uint32_t r = lo;
+      for (uint32_t i = lo; i < hi; i++) r += S.keys[i] < kv[j];
+      rk[j] = r;
+    }
+  }
+  team_sync<NT>();
+#pragma unroll
+  for (int j = 0; j < KPL; j++)
+    if (j * NT + tid < n) S.keys[rk[j]] = kv[j];
+  team_sync<NT>();
+  return true;
+}
+
 // Inclusive prefix moments P(i) of the blob's points: the owning chunk's base
 // plus the chunk's words up to i.  Called by every lane of the team (the base
 // of a wave-sized team comes by lane shuffle); inactive lanes get zero.
@@ -1736,17 +1846,23 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k]);
   // the accumulators live in the team's LDS, not in registers
   if (prm.probe && tid == 0) S.t_last = S.t_item = wall_clock64();
+  bool big = false;
   auto phase = [&](int k) {  // accumulated per team, flushed once per kernel
     if (prm.probe && tid == 0) {
       const uint64_t now = wall_clock64();
       pacc[k] += (uint32_t)(now - S.t_last);
       pacc[10 + k] += 1;
+      if (NT > 64 && big) {  // the few very large blobs (> 2048 points) separately: probe[208 + k], count [220]
+        atomicAdd((unsigned long long*)&b.probe[208 + k], (unsigned long long)(now - S.t_last));
+        if (k == 0) atomicAdd((unsigned long long*)&b.probe[220], 1ull);
+      }
       S.t_last = now;
     }
   };
   const int f = (int)(w >> 16);
   const uint32_t rank = w & 0xffff;
   const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+  big = n > 2048;
   const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
 
@@ -1755,14 +1871,21 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
   const uint32_t bi = rank & 0xfff;
   phase(0);
-  bool sorted = false;
+  bool sorted = false, in_lds = false;
   if constexpr (NT == 64) {
     if (n >= 64) {  // keys go straight from global memory into registers
       phase(1);
       sorted = wave_bucket_sort<CAP>(S, grp, (int)n);
+      in_lds = true;
+    }
+  } else if constexpr (CAP / NT <= 16) {
+    if (n >= 64) {
+      phase(1);
+      sorted = team_reg_bucket_sort<NT, CAP>(S, grp, (int)n);
+      in_lds = true;
     }
   }
-  if (!sorted && (NT != 64 || n < 64)) {
+  if (!sorted && !in_lds) {
     for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
     phase(1);
     team_sync<NT>();
@@ -1878,11 +2001,33 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   team_sync<NT>();
   const uint32_t npk = S.npeaks;
   {
-    int p2 = 2;
-    while (p2 < (int)npk) p2 <<= 1;
-    for (int t = (int)npk + tid; t < p2; t += NT) pk_put<kGlobPk>(pks, gpk, kPk, t, ~0ull);
+    // FitQuads reads only the first min(10, npk) entries of the peak order (P9
+    // sorts all of a blob's peaks): select them -- 10 rounds of a team minimum
+    // over the keys (unique: the point index is in the low word) above the
+    // previous pick -- instead of sorting every peak
+    constexpr int kPP = (CAP / 2 + NT - 1) / NT;  // a cyclic sequence of n has <= n/2 strict maxima
+    uint64_t mine[kPP];
+#pragma unroll
+    for (int j = 0; j < kPP; j++) {
+      const int t = j * NT + tid;
+      mine[j] = t < (int)npk ? pk_get<kGlobPk>(pks, gpk, kPk, t) : ~0ull;
+    }
+    const int ntop = npk < (uint32_t)kNMaxima ? (int)npk : kNMaxima;
+    uint64_t* red = reinterpret_cast<uint64_t*>(S.red_f64);
+    uint64_t last = 0;
+    team_sync<NT>();  // every peak read before slots 0..9 are rewritten
+    for (int r = 0; r < ntop; r++) {
+      uint64_t m = ~0ull;
+#pragma unroll
+      for (int j = 0; j < kPP; j++) {
+        const uint64_t k = mine[j];
+        if ((r == 0 || k > last) && k < m) m = k;
+      }
+      m = team_reduce<NT>(m, MinOp(), red);
+      if (tid == 0) pks[r] = m;
+      last = m;
+    }
     team_sync<NT>();
-    if (npk > 1) team_bitonic_sort_pk<NT, kGlobPk>(pks, gpk, kPk, p2);
   }
   phase(5);
   if (prm.diag_stop == 4) return;

@@ -38,3 +38,7 @@ for kind, base in (("small", 64), ("large", 80), ("decode", 128)):
 for name, idx in (("small", 200), ("large", 201)):
     v = int(det.copy_probe().astype(np.int64)[idx])
     print("slowest %s item: %.2f us, %d points" % (name, (v >> 20) / 100.0, v & 0xfffff))
+pp = det.copy_probe().astype(np.int64)
+nbig = max(1, int(pp[220]) // 2)
+print("large blobs > 2048 points (%d per batch): mean phase us" % nbig,
+      [round(pp[208 + k] / 100.0 / 2 / nbig, 2) for k in range(10)])
