@@ -669,9 +669,9 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   for (int f = 0; f < d->last_nframes; f++) {
     v[1] += d->h_ctrl[kCtlNpts * B + f];
     v[2] += d->h_ctrl[kCtlNpairs * B + f];
-    v[5] += d->h_ctrl[kCtlNquads * B + f];
     v[6] += d->h_ctrl[kCtlNdets * B + f];
   }
+  v[5] = d->h_ctrl[kCtlNquads * B];  // FitQuads records of the batch (counted per blob team)
   v[3] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts];
   v[4] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts + 1];
   const int n = std::min(cap, 7);

@@ -1407,7 +1407,9 @@ struct BlobShared {
   uint32_t item, nwork, npeaks;
   int32_t pi[16];
   double lines[4][4];
-  uint32_t pacc[21];  // probe accumulators + processed-point count of this team
+  uint32_t pacc[22];  // probe accumulators + processed-point and FitQuads counts of this team
+  uint32_t ph[10];    // probe: phase durations of the current item
+  uint32_t slow_dt, slow_n, slow_ph[10];  // probe: this team's slowest item
   uint64_t t_last, t_item;
 };
 
@@ -1849,8 +1851,10 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   bool big = false;
   auto phase = [&](int k) {  // accumulated per team, flushed once per kernel
     if (prm.probe && tid == 0) {
+      if (k == 9) __builtin_amdgcn_s_waitcnt(0);  // the item's stores are acknowledged inside its own time
       const uint64_t now = wall_clock64();
       pacc[k] += (uint32_t)(now - S.t_last);
+      S.ph[k] = (uint32_t)(now - S.t_last);
       pacc[10 + k] += 1;
       if (NT > 64 && big) {  // the few very large blobs (> 2048 points) separately: probe[208 + k], count [220]
         atomicAdd((unsigned long long*)&b.probe[208 + k], (unsigned long long)(now - S.t_last));
@@ -1865,9 +1869,12 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   big = n > 2048;
   const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
+  const uint32_t sel = b.pair_sel[(size_t)f * kMaxPairs + rank];
+  // the three loads in one round trip: n and off are needed before the branch
+  asm volatile("" ::"v"(n), "v"(off));
 
   // extents, SelectBlobs and the theta keys come from k_extents
-  if (b.pair_sel[(size_t)f * kMaxPairs + rank] == 0) return;  // uniform across the team
+  if (sel == 0) return;  // uniform across the team
   if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
   const uint32_t bi = rank & 0xfff;
   phase(0);
@@ -2202,7 +2209,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     }
     rec.accepted = ok;
     b.quads[(size_t)f * kMaxPairs + rank] = rec;  // slot = pair rank: no returning atomic
-    atomicAdd(b.nquads + f, 1u);                  // count only (result unused: fire and forget)
+    pacc[21] += 1;  // FitQuads records of this team (batch statistics, one atomic per team at the end)
     if (ok && prm.diag_stop != 5) {
       qcand.frame = (uint32_t)f;
       qcand.rank = rank;
@@ -2212,9 +2219,14 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     }
   }
   phase(9);
-  if (prm.probe && tid == 0)  // slowest item of the kernel: (wall-clock ticks << 20) | points
-    atomicMax((unsigned long long*)&b.probe[NT == 64 ? 200 : 201],
-              (unsigned long long)(((S.t_last - S.t_item) << 20) | n));
+  if (prm.probe && tid == 0) {  // slowest item of this team (flushed at kernel end): ticks, points, phases
+    const uint32_t dt = (uint32_t)(S.t_last - S.t_item);
+    if (dt > S.slow_dt) {
+      S.slow_dt = dt;
+      S.slow_n = n;
+      for (int k = 0; k < 10; k++) S.slow_ph[k] = S.ph[k];
+    }
+  }
   team_sync<NT>();
 }
 
@@ -2386,6 +2398,19 @@ __global__ __launch_bounds__(256) void k_extents(DevBufs b, Geom g) {
   }
 }
 
+// slowest item over the teams: probe[200 | 201] = (ticks << 20) | points; the
+// phases of the slowest small item of each team summed in probe[224 + k], [234] teams
+template <int NT, int CAP>
+__device__ __forceinline__ void probe_flush_slow(const DevBufs& b, const Params& prm, const BlobShared<NT, CAP>& S,
+                                                 bool leader) {
+  if (!prm.probe || !leader || !S.slow_dt) return;
+  atomicMax((unsigned long long*)&b.probe[NT == 64 ? 200 : 201], ((unsigned long long)S.slow_dt << 20) | S.slow_n);
+  if (NT == 64) {
+    for (int k = 0; k < 10; k++) atomicAdd((unsigned long long*)&b.probe[224 + k], (unsigned long long)S.slow_ph[k]);
+    atomicAdd((unsigned long long*)&b.probe[234], 1ull);
+  }
+}
+
 __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm, const uint32_t* pacc, int base,
                                             bool leader) {
   if (!prm.probe || !leader) return;
@@ -2402,7 +2427,8 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
   uint32_t* pacc = S.pacc;
-  if (tid < 21) pacc[tid] = 0;
+  if (tid < 22) pacc[tid] = 0;
+  if (tid == 0) S.slow_dt = 0;
   uint64_t* gpk = b.s_pk + (size_t)blockIdx.x * (kSortCap / 2);
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, tid, NT);
@@ -2424,7 +2450,9 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   }
   __syncthreads();
   probe_flush(b, prm, pacc, 80, tid == 0);
+  probe_flush_slow(b, prm, S, tid == 0);
   if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
+  if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
@@ -2437,7 +2465,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t lane = lane_id();
   BlobShared<64, kSmallBlob>& S = Ss[wave];
   uint32_t* pacc = S.pacc;
-  if (lane < 21) pacc[lane] = 0;
+  if (lane < 22) pacc[lane] = 0;
+  if (lane == 0) S.slow_dt = 0;
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, threadIdx.x, 256);
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
@@ -2454,7 +2483,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     blob_item<64, kSmallBlob>(b, g, prm, S, nullptr, s_combo, w, pacc);
   }
   probe_flush(b, prm, pacc, 64, lane == 0);
+  probe_flush_slow(b, prm, S, lane == 0);
   if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
+  if (lane == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
 }
 
 // ---------------------------------------------------------------------------

@@ -42,3 +42,6 @@ pp = det.copy_probe().astype(np.int64)
 nbig = max(1, int(pp[220]) // 2)
 print("large blobs > 2048 points (%d per batch): mean phase us" % nbig,
       [round(pp[208 + k] / 100.0 / 2 / nbig, 2) for k in range(10)])
+nslow = max(1, int(pp[234]))
+print("slowest small item per wave team (%d teams): mean phase us" % int(pp[234]),
+      [round(pp[224 + k] / 100.0 / nslow, 2) for k in range(10)])
