@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
     ap.add_argument("--pool", type=int, default=64, help="distinct synthetic frames per GPU")
+    ap.add_argument("--hbm-copies", type=int, default=4,
+                    help="copies of the frame pool in HBM (4 x 64 frames = 0.47 GB at 720p, more than the "
+                         "256 MB Infinity Cache, so the timed steps read their frames from HBM)")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--tags", type=int, default=15)
@@ -163,10 +166,11 @@ def main():
     assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
     scatter = args.ingest == "scatter"
     frames = render_pool(args, rank)
-    d_frames = torch.from_numpy(frames).to("cuda")
+    copies = 1 if args.ingest == "scatter" else max(1, args.hbm_copies)
+    d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
-    npool = args.pool
+    npool = args.pool * copies
     dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank) for _ in range(args.instances)]
     ingest = None
     if scatter:
@@ -298,10 +302,10 @@ def main():
     if args.latency_frames > 0:
         lat_det = rva.GpuDetector(W, H, max_batch=1, device=local_rank)
         for i in range(10):
-            lat_det.detect_count(frames[i % npool])
+            lat_det.detect_count(frames[i % args.pool])
             lat_det.detect_device(base + (i % npool) * stride, stride, 1, counts_only=True)
         for i in range(args.latency_frames):
-            fr = frames[i % npool]
+            fr = frames[i % args.pool]
             t1 = time.perf_counter()
             lat_det.detect_count(fr)
             lat_h.append(time.perf_counter() - t1)
@@ -343,7 +347,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": "configs[1]: 1280x720 single-camera synthetic tag36h11 stream "
                                "(%d tags/frame, YUYV, frames resident in HBM)" % args.tags,
-                   "width": W, "height": H, "batch_per_gpu": B, "distinct_frames_per_gpu": npool,
+                   "width": W, "height": H, "batch_per_gpu": B, "distinct_frames_per_gpu": args.pool,
+                   "frames_resident_per_gpu": npool,
                    "parallelism": ("frame-sharded x%d, frames scattered from rank 0 over RCCL, records gathered "
                                    "to rank 0" % world) if scatter else
                                   "frame-sharded x%d (no data-path collective)" % world,
