@@ -2503,10 +2503,19 @@ __constant__ float c_border_pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0,
 // cos / sin of rot * pi/2 as libm returns them (quad_decode's rotation of H)
 __constant__ double c_rot_c[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
 __constant__ double c_rot_s[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
+// Refine samples of one quad: 4 edges of max(16, len / 8) samples, so at most
+// perimeter / 8 + 64 for a quad inside the frame (perimeter <= 2 (W + H)).  The
+// LDS sample buffer is sized by the geometry (768 covers 720p, 1024 1080p,
+// 1536 every frame the reference admits): a 17 KB workgroup instead of 29 KB
+// keeps 8 quads per CU in flight.
 constexpr int kMaxRefineSamples = 1536;
+__host__ __device__ constexpr int refine_cap_for(int W, int H) {
+  return (2 * (W + H) + 7) / 8 + 64 <= 768 ? 768 : ((2 * (W + H) + 7) / 8 + 64 <= 1024 ? 1024 : kMaxRefineSamples);
+}
 
+template <int RCAP>
 struct DecodeShared {
-  double sx[kMaxRefineSamples], sy[kMaxRefineSamples];
+  double sx[RCAP], sy[RCAP];
   float qc[4][2];
   int nsamp[4], samp_off[4];
   float enx[4], eny[4];
@@ -2524,8 +2533,9 @@ struct DecodeShared {
   uint32_t qpre[kMaxBatch + 1];
 };
 
+template <int RCAP>
 __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm, int B) {
-  __shared__ DecodeShared S;
+  __shared__ DecodeShared<RCAP> S;
   const int tid = threadIdx.x;
   // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
   uint32_t* qpre = S.qpre;
@@ -2585,7 +2595,8 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         for (int k = 0; k < 4; k++) { S.samp_off[k] = acc; acc += S.nsamp[k]; }
       }
       __syncthreads();
-      const int total = min(S.samp_off[3] + S.nsamp[3], kMaxRefineSamples);
+      const int total = min(S.samp_off[3] + S.nsamp[3], RCAP);
+      if (tid == 0 && S.samp_off[3] + S.nsamp[3] > RCAP) atomicOr(b.status + f, kStatusQuadsOverflow);
       for (int t = tid; t < total; t += kDecodeThreads) {
         int edge = 0;
         while (edge < 3 && t >= S.samp_off[edge + 1]) edge++;
@@ -2640,7 +2651,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       if (tid < 4) {
         double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
         const int o = S.samp_off[tid];
-        for (int s = 0; s < S.nsamp[tid] && o + s < kMaxRefineSamples; s++) {
+        for (int s = 0; s < S.nsamp[tid] && o + s < RCAP; s++) {
           const double bx = S.sx[o + s], by = S.sy[o + s];
           if (isnan(bx)) continue;
           Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
@@ -2988,7 +2999,15 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }
   tk(10, st, 0);
-  hipLaunchKernelGGL(k_decode, dim3(nblobwg * 2), dim3(kDecodeThreads), 0, st, b, g, prm, B);
+  {
+    // one wave per workgroup, persistent over the accepted quads: enough groups
+    // for every quad of a full batch to start at once (8 per CU at 17 KB LDS)
+    const dim3 grd(std::max(nblobwg * 2, std::min(nblobwg * 4, 64 * B)));
+    const int rcap = refine_cap_for(g.W, g.H);
+    if (rcap == 768) hipLaunchKernelGGL(k_decode<768>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+    else if (rcap == 1024) hipLaunchKernelGGL(k_decode<1024>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+    else hipLaunchKernelGGL(k_decode<kMaxRefineSamples>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+  }
   tk(10, st, 1);
   mark();
   tk(11, st, 0);
