@@ -458,16 +458,45 @@ __device__ void g_union(uint32_t* par, uint32_t a, uint32_t b) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
+// Union of the components of a and b with both finds advanced in lockstep (their
+// loads issued together), links by atomicMin to the smaller id as in g_union.
+__device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    uint32_t pa = g_load(par + a), pb = g_load(par + b);
+    while (pa != a || pb != b) {
+      a = pa;
+      b = pb;
+      pa = g_load(par + a);
+      pb = g_load(par + b);
+    }
+    if (a == b) return;
+    if (a < b) {
+      const uint32_t old = atomicMin(par + b, a);
+      if (old == b) return;
+      b = old;
+    } else {
+      const uint32_t old = atomicMin(par + a, b);
+      if (old == a) return;
+      a = old;
+    }
+  }
+}
+
+// One candidate union per thread (the reference's Merge, labeling_allegretti_2019_BKE.cu:302-338,
+// over the tile's border blocks): threads 0-79 the top block row (16 blocks x
+// P, Q, R and the two background links), 80-127 the left block column (16 x P,
+// S, background S), 128-142 the right column (15 x R).  Every union is one
+// short chain of global round trips instead of up to five in a row per lane.
+constexpr int kBorderThreads = 192;
+__global__ __launch_bounds__(kBorderThreads) void k_ccl_border(DevBufs b, Geom g) {
   const int f = blockIdx.z;
-  const int lane = threadIdx.x;
-  const int tile_x = blockIdx.x, tile_y = blockIdx.y;
-  int bty, btx, role;
-  if (lane < 16) { role = 0; bty = 0; btx = lane; }
-  else if (lane < 32) { role = 1; bty = lane - 16; btx = 0; }
-  else if (lane < 47) { role = 2; bty = lane - 31; btx = 15; }
+  const int t = threadIdx.x;
+  int bty, btx, role, kind;
+  if (t < 80) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
+  else if (t < 128) { role = 1; bty = (t - 80) / 3; btx = 0; kind = (t - 80) % 3; }
+  else if (t < 143) { role = 2; bty = t - 127; btx = 15; kind = 0; }
   else return;
-  const int BY = tile_y * 16 + bty, BX = tile_x * 16 + btx;
+  const int BY = blockIdx.y * 16 + bty, BX = blockIdx.x * 16 + btx;
   if (BY >= g.BH || BX >= g.BW) return;
   const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -480,22 +509,30 @@ __global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
   };
   const uint8_t a = thr[idx], bb = thr[idx + 1], c = thr[idx + Wd];
   const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
+  uint32_t u = 0, v = 0;
+  bool link = false;
   if (role == 0 && BY > 0) {
-    if (a == 255 && px(row - 1, col - 1) == 255) g_union(par, F, F - 2 * Wd - 2);
-    if ((a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255))
-      g_union(par, F, F - 2 * Wd);
-    if (bb == 255 && px(row - 1, col + 2) == 255) g_union(par, F, F - 2 * Wd + 2);
-    if (a == 0 && px(row - 1, col) == 0) g_union(par, L, L - 2 * Wd);
-    if (bb == 0 && px(row - 1, col + 1) == 0) g_union(par, R, R - 2 * Wd);
+    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255);
+      u = F; v = F - 2 * Wd;
+    }
+    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2; }
+    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - 2 * Wd; }
+    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - 2 * Wd; }
+  } else if (role == 1 && BX > 0) {
+    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255);
+      u = F; v = F - 2;
+    } else {
+      link = (a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0);
+      u = L; v = L - 1;
+    }
+  } else if (role == 2 && BY > 0) {
+    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
   }
-  if (role == 1 && BX > 0) {
-    if (BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255) g_union(par, F, F - 2 * Wd - 2);
-    if ((a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255)) g_union(par, F, F - 2);
-    if ((a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0)) g_union(par, L, L - 1);
-  }
-  if (role == 2 && BY > 0) {
-    if (bb == 255 && px(row - 1, col + 2) == 255) g_union(par, F, F - 2 * Wd + 2);
-  }
+  if (link) g_union2(par, u, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -2939,7 +2976,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(1, st, 1);
     mark();
     tk(2, st, 0);
-    hipLaunchKernelGGL(k_ccl_border, grd, dim3(64), 0, st, b, g);
+    hipLaunchKernelGGL(k_ccl_border, grd, dim3(kBorderThreads), 0, st, b, g);
     tk(2, st, 1);
     mark();
   }
