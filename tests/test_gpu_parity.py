@@ -280,3 +280,37 @@ def test_distortion_variants(gpu, oracle_mod, dist):
     assert compare_frame(det, orc) == []
     assert compare_detections(dets, orc.detections()) == []
     assert sorted(d.id for d in dets) == sorted(t[0] for t in truth)
+
+
+@pytest.mark.parametrize("batch,timed", [(8, "k_blob"), (8, "k_boundary"), (1, "k_blob_small"), (1, "k_pose")])
+def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
+    """The bench's launch modes give identical detections: hipGraph replay, the
+    split graph around a timed kernel (fence-free events between three graphs; on
+    the fork branch at B < 8 a direct launch), and stage profiling (direct
+    launches with events between every kernel).  The timer reports every launch."""
+    import torch
+    from ros_vision_amd import synth
+    frames = np.stack([synth.stream_frame(1280, 720, 20 + i)[0] for i in range(batch)])
+    t = torch.from_numpy(frames).cuda()
+    det = gpu.GpuDetector(1280, 720, max_batch=batch)
+
+    def run(n=2):
+        out = None
+        for _ in range(n):
+            det.enqueue_device(t.data_ptr(), frames[0].nbytes, batch)
+            det.collect(counts_only=True)
+            out = [[(d.id, tuple(np.round(d.p.ravel(), 9))) for d in det._unpack(batch)[f]] for f in range(batch)]
+        return out
+
+    base = run()
+    det.set_kernel_timer(timed)
+    assert run(3) == base
+    ms, launches = det.kernel_time()
+    assert launches == 3 and ms > 0
+    det.set_kernel_timer(None)
+    det.set_profiling(True)
+    assert run() == base
+    stages, nb = det.stage_times()
+    det.set_profiling(False)
+    assert nb >= 2 and all(v > 0 for v in stages.values())
+    assert run() == base
