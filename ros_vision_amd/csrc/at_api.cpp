@@ -321,9 +321,15 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
   d->poses.assign(B * kMaxDets, at_pose{});
   d->nposes.assign(B, 0);
-  if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
-  if (hipHostMalloc((void**)&d->h_dets, B * kMaxDets * sizeof(DevDetection), hipHostMallocDefault) != hipSuccess)
+  if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocMapped) != hipSuccess) return fail(AT_E_NOMEM);
+  if (hipHostMalloc((void**)&d->h_dets, B * kMaxDets * sizeof(DevDetection), hipHostMallocMapped) != hipSuccess)
     return fail(AT_E_NOMEM);
+  // device views of the mapped host result buffers (k_decode / k_pose write them)
+  if (hipHostGetDevicePointer((void**)&b.hdets, d->h_dets, 0) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&b.hctrl, d->h_ctrl, 0) != hipSuccess)
+    return fail(AT_E_HIP);
+  b.ctrl = d->d_ctrl;
+  b.ctrl_words = (uint32_t)d->ctrl_words;
   {
     std::vector<uint64_t> codes(kTag36h11Known);
     std::vector<int> ids(kTag36h11Known);
@@ -427,14 +433,19 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
 static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev,
                                   const KernelTimer* kt) {
   hipError_t e;
+  // AT_DIAG_NOCOPY=4 (timing experiments only; host results then stale): no
+  // control-block copy-out when k_pose does not run
+  static const int diag_nocopy = getenv("AT_DIAG_NOCOPY") ? (atoi(getenv("AT_DIAG_NOCOPY")) & 4) : 0;
   if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
   if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
   if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
                            kt)))
     return e;
-  if ((e = hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st))) return e;
-  return hipMemcpyAsync(d->h_dets, d->d.dets, (size_t)nframes * kMaxDets * sizeof(DevDetection),
-                        hipMemcpyDeviceToHost, st);
+  // results reach the host zero-copy: k_decode writes the detections into the
+  // mapped host buffer and k_pose adds the poses and the control block; without
+  // k_pose (tag_size == 0) the control block is copied here
+  if (d->prm.tag_size > 0 || (diag_nocopy & 4)) return hipSuccess;
+  return hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st);
 }
 
 // KernelTimer::split hook while capturing: close the current segment, open the next

@@ -150,6 +150,14 @@ struct DevBufs {
   uint32_t* work;     // [kNumCls][wcap] (frame << 16) | rank of candidate pairs, by size class
   uint32_t wcap;      // B * kMaxPairs
   DevDetection* dets; // [B][kMaxDets]
+  // zero-copy results: the detections (k_decode, poses added by k_pose) and the
+  // control block (copied by k_pose) are also written straight into the
+  // caller-visible pinned host buffers (device pointers of mapped host memory),
+  // which replaces two device-to-host copies per batch
+  DevDetection* hdets;  // [B][kMaxDets] host
+  uint32_t* hctrl;      // [ctrl_words] host
+  uint32_t* ctrl;       // device control block base
+  uint32_t ctrl_words;
   QuadRecord* quads;  // [B][kMaxPairs]  fitted-quad debug record of each kept blob, slot = pair rank
   // control block (zeroed every batch)
   uint32_t* npts;     // [B]

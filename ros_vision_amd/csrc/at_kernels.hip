@@ -2884,7 +2884,10 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
           hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
         }
         const uint32_t di = atomicAdd(b.ndets + f, 1u);
-        if (di < (uint32_t)kMaxDets) b.dets[(size_t)f * kMaxDets + di] = d;
+        if (di < (uint32_t)kMaxDets) {
+          b.dets[(size_t)f * kMaxDets + di] = d;
+          b.hdets[(size_t)f * kMaxDets + di] = d;  // pose fields follow from k_pose
+        }
         else atomicOr(b.status + f, kStatusDetsOverflow);
       }
     }
@@ -2920,6 +2923,10 @@ __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
   const int f = blockIdx.y;
   const uint32_t i = blockIdx.x * (64 / kPoseLanes) + threadIdx.x / kPoseLanes;
   const int sub = (int)(threadIdx.x % kPoseLanes);
+  // the control block is final once k_decode has finished: block (0, 0) hands it
+  // to the host (replaces a device-to-host copy)
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (uint32_t w = threadIdx.x; w < b.ctrl_words; w += 64) b.hctrl[w] = b.ctrl[w];
   const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
   if (i >= n) return;  // uniform across the quad
   DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
@@ -2927,12 +2934,13 @@ __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
   pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
                           (prm.probe && f == 0 && i == 0 && sub == 0) ? b.probe + 16 : nullptr);
   if (sub == 0) {
+    DevDetection& h = b.hdets[(size_t)f * kMaxDets + i];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d.pose_R[k] = R[k];
+    for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
 #pragma unroll
-    for (int k = 0; k < 3; k++) d.pose_t[k] = t[k];
-    d.pose_err[0] = err[0];
-    d.pose_err[1] = err[1];
+    for (int k = 0; k < 3; k++) d.pose_t[k] = h.pose_t[k] = t[k];
+    d.pose_err[0] = h.pose_err[0] = err[0];
+    d.pose_err[1] = h.pose_err[1] = err[1];
   }
 }
 
