@@ -60,8 +60,7 @@ struct at_detector {
   std::vector<void*> allocs;
   uint8_t* d_in;            // staging for host frames [B][max frame bytes]
   size_t in_stride;
-  const uint8_t** d_ftab;   // device frame pointer table
-  const uint8_t** h_ftab;   // pinned
+  const uint8_t** h_ftab;   // frame pointer table (mapped, fine-grained host memory; k_pre reads it)
   uint32_t* d_ctrl;         // control block (zeroed each batch)
   size_t ctrl_words;
   uint32_t* h_ctrl;         // pinned copy of the control block
@@ -265,9 +264,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   };
   d->in_stride = (npix * 3 + 255) & ~(size_t)255;
   d->d_in = (uint8_t*)dalloc(B * d->in_stride);
-  d->d_ftab = (const uint8_t**)dalloc(B * sizeof(void*));
   DevBufs& b = d->d;
-  b.frames = d->d_ftab;
   b.gray = (uint8_t*)dalloc(B * npix);
   b.dec = (uint8_t*)dalloc(B * nd);
   b.mm = (uint8_t*)dalloc(B * nt);
@@ -318,7 +315,11 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)
   b.s_pk = (uint64_t*)dalloc((size_t)d->nblobwg * (kSortCap / 2) * 8);
   if (oom) return fail(AT_E_NOMEM);
-  if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocDefault) != hipSuccess) return fail(AT_E_NOMEM);
+  // frame pointer table: fine-grained mapped host memory read by k_pre directly
+  // (no host-to-device copy per batch; the GPU does not cache it)
+  if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return fail(AT_E_NOMEM);
+  if (hipHostGetDevicePointer((void**)&b.frames, (void*)d->h_ftab, 0) != hipSuccess) return fail(AT_E_HIP);
   d->poses.assign(B * kMaxDets, at_pose{});
   d->nposes.assign(B, 0);
   if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocMapped) != hipSuccess) return fail(AT_E_NOMEM);
@@ -436,7 +437,6 @@ static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStrea
   // AT_DIAG_NOCOPY=4 (timing experiments only; host results then stale): no
   // control-block copy-out when k_pose does not run
   static const int diag_nocopy = getenv("AT_DIAG_NOCOPY") ? (atoi(getenv("AT_DIAG_NOCOPY")) & 4) : 0;
-  if ((e = hipMemcpyAsync((void*)d->d_ftab, d->h_ftab, nframes * sizeof(void*), hipMemcpyHostToDevice, st))) return e;
   if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
   if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
                            kt)))
@@ -590,6 +590,7 @@ int at_detect_batch(at_detector* d, const uint8_t* const* frames, int nframes, a
                     int cap_per_frame, int* n_per_frame) {
   if (!d || !frames || nframes < 1 || nframes > d->B || !check_fmt(fmt)) return AT_E_INVALID;
   HIPCHK(hipSetDevice(d->device));
+  if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));  // the frame table is read by the pending batch
   const size_t fb = frame_bytes(d, fmt);
   for (int f = 0; f < nframes; f++) {
     HIPCHK(hipMemcpyAsync(d->d_in + (size_t)f * d->in_stride, frames[f], fb, hipMemcpyHostToDevice, d->st));
