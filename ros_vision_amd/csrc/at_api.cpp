@@ -437,7 +437,6 @@ static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStrea
   // AT_DIAG_NOCOPY=4 (timing experiments only; host results then stale): no
   // control-block copy-out when k_pose does not run
   static const int diag_nocopy = getenv("AT_DIAG_NOCOPY") ? (atoi(getenv("AT_DIAG_NOCOPY")) & 4) : 0;
-  if ((e = hipMemsetAsync(d->d_ctrl, 0, d->ctrl_words * 4, st))) return e;
   if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
                            kt)))
     return e;

@@ -167,6 +167,10 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
   const int f = blockIdx.z;
   const int tx = blockIdx.x * 64 + threadIdx.x;
   const int ty = blockIdx.y * 4 + threadIdx.y;
+  // the batch's control block starts at zero (no memset node): nothing in k_pre
+  // reads it, every later kernel follows in stream order
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+    for (uint32_t w = threadIdx.y * 64 + threadIdx.x; w < b.ctrl_words; w += 256) b.ctrl[w] = 0;
   if (tx >= g.TW || ty >= g.TH) return;
   const uint8_t* in = b.frames[f];
   uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
