@@ -2197,50 +2197,75 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     S.lines[tid][3] = o.p23[1];
   }
   team_sync<NT>();
-  if (tid == 0) {
-    QuadRecord rec;
-    rec.blob_index = bi;
-    rec.valid = valid;
-    for (int k = 0; k < 4; k++) rec.indices[k] = qidx[k];
-    float qc[4][2];
-    int ok = valid;
-    for (int k = 0; ok && k < 4; k++) {
-      const int k1 = (k + 1) & 3;
+  // the four corners (lanes 0-3), the six Heron sides (lanes 0-5) and the four
+  // corner angles (lanes 0-3) of wave 0 in parallel, each with the reference's
+  // float / double expression; the record is then written by lane 0
+  if (tid < 64) {
+    const uint32_t ln = lane_id();
+    float cxk = 0.f, cyk = 0.f;
+    bool cok = true;
+    if (valid && ln < 4) {
+      const int k = (int)ln, k1 = (k + 1) & 3;
       const double A00 = S.lines[k][3], A01 = -S.lines[k1][3];
       const double A10 = -S.lines[k][2], A11 = S.lines[k1][2];
       const double B0 = -S.lines[k][0] + S.lines[k1][0];
       const double B1 = -S.lines[k][1] + S.lines[k1][1];
       const double det = A00 * A11 - A10 * A01;
       const double W00 = A11 / det, W01 = -A01 / det;
-      if (fabs(det) < 0.001) { ok = 0; break; }
-      const double L0 = W00 * B0 + W01 * B1;
-      qc[k][0] = (float)(S.lines[k][0] + L0 * A00);
-      qc[k][1] = (float)(S.lines[k][1] + L0 * A10);
+      cok = !(fabs(det) < 0.001);
+      if (cok) {
+        const double L0 = W00 * B0 + W01 * B1;
+        cxk = (float)(S.lines[k][0] + L0 * A00);
+        cyk = (float)(S.lines[k][1] + L0 * A10);
+      }
+    }
+    int ok = valid && __ballot(ln < 4 && !cok) == 0;
+    float qc[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      qc[k][0] = wave_read(cxk, k);
+      qc[k][1] = wave_read(cyk, k);
     }
     if (ok) {
-      float area = 0, len[3], pp;
-      for (int k = 0; k < 3; k++) {
-        const int a2 = k, b2 = (k + 1) % 3;
-        len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+      // sides of triangles (0,1,2) and (2,3,0): 0->1, 1->2, 2->0, 2->3, 3->0, 0->2
+      float lj = 0.f;
+      if (ln < 6) {
+        const int a2 = ln == 0 ? 0 : ln == 1 ? 1 : ln == 2 ? 2 : ln == 3 ? 2 : ln == 4 ? 3 : 0;
+        const int b2 = ln == 0 ? 1 : ln == 1 ? 2 : ln == 2 ? 0 : ln == 3 ? 3 : ln == 4 ? 0 : 2;
+        const float xa = a2 == 0 ? qc[0][0] : a2 == 1 ? qc[1][0] : a2 == 2 ? qc[2][0] : qc[3][0];
+        const float ya = a2 == 0 ? qc[0][1] : a2 == 1 ? qc[1][1] : a2 == 2 ? qc[2][1] : qc[3][1];
+        const float xb = b2 == 0 ? qc[0][0] : b2 == 1 ? qc[1][0] : b2 == 2 ? qc[2][0] : qc[3][0];
+        const float yb = b2 == 0 ? qc[0][1] : b2 == 1 ? qc[1][1] : b2 == 2 ? qc[2][1] : qc[3][1];
+        lj = det_hypotf(xb - xa, yb - ya);
       }
+      float len[6];
+#pragma unroll
+      for (int j = 0; j < 6; j++) len[j] = wave_read(lj, j);
+      float area = 0, pp;
       pp = (len[0] + len[1] + len[2]) / 2;
       area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
-      const int idxs[4] = {2, 3, 0, 2};
-      for (int k = 0; k < 3; k++) {
-        const int a2 = idxs[k], b2 = idxs[k + 1];
-        len[k] = det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
-      }
-      pp = (len[0] + len[1] + len[2]) / 2;
-      area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+      pp = (len[3] + len[4] + len[5]) / 2;
+      area += sqrtf(pp * (pp - len[3]) * (pp - len[4]) * (pp - len[5]));
       if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = 0;
     }
-    for (int k = 0; ok && k < 4; k++) {
-      const int i0 = k, i1 = (k + 1) & 3, i2 = (k + 2) & 3;
-      const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
-      const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
-      const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
-      if ((double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2) ok = 0;
+    if (ok) {
+      bool abad = false;
+      if (ln < 4) {
+        const int i0 = (int)ln, i1 = (i0 + 1) & 3, i2 = (i0 + 2) & 3;
+        auto cx = [&](int i) { return i == 0 ? qc[0][0] : i == 1 ? qc[1][0] : i == 2 ? qc[2][0] : qc[3][0]; };
+        auto cy = [&](int i) { return i == 0 ? qc[0][1] : i == 1 ? qc[1][1] : i == 2 ? qc[2][1] : qc[3][1]; };
+        const float dx1 = cx(i1) - cx(i0), dy1 = cy(i1) - cy(i0);
+        const float dx2 = cx(i2) - cx(i1), dy2 = cy(i2) - cy(i1);
+        const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
+        abad = (double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2;
+      }
+      if (__ballot(abad)) ok = 0;
     }
+  if (ln == 0) {
+    QuadRecord rec;
+    rec.blob_index = bi;
+    rec.valid = valid;
+    for (int k = 0; k < 4; k++) rec.indices[k] = qidx[k];
     QuadCand qcand;
     for (int k = 0; k < 4; k++) {  // AdjustPixelCenters, quad_decimate 2
       const float x = ok ? (qc[k][0] - 0.5f) * 2.0f + 0.5f : 0.f;
@@ -2258,6 +2283,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       if (ci < (uint32_t)kQuadCandPerFrame) b.qcand[(size_t)f * kQuadCandPerFrame + ci] = qcand;
       else atomicOr(b.status + f, kStatusQuadsOverflow);
     }
+  }
   }
   phase(9);
   if (prm.probe && tid == 0) {  // slowest item of this team (flushed at kernel end): ticks, points, phases
