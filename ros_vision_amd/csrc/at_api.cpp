@@ -434,16 +434,13 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
 static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev,
                                   const KernelTimer* kt) {
   hipError_t e;
-  // AT_DIAG_NOCOPY=4 (timing experiments only; host results then stale): no
-  // control-block copy-out when k_pose does not run
-  static const int diag_nocopy = getenv("AT_DIAG_NOCOPY") ? (atoi(getenv("AT_DIAG_NOCOPY")) & 4) : 0;
   if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
                            kt)))
     return e;
   // results reach the host zero-copy: k_decode writes the detections into the
   // mapped host buffer and k_pose adds the poses and the control block; without
   // k_pose (tag_size == 0) the control block is copied here
-  if (d->prm.tag_size > 0 || (diag_nocopy & 4)) return hipSuccess;
+  if (d->prm.tag_size > 0) return hipSuccess;
   return hipMemcpyAsync(d->h_ctrl, d->d_ctrl, d->ctrl_words * 4, hipMemcpyDeviceToHost, st);
 }
 
