@@ -25,4 +25,7 @@ def test_reference_fixture_expectations():
     assert [d["id"] for d in VEC["colorimage"]["detections"]] == [554]
     assert VEC["colorimage_notags"]["detections"] == []
     assert [d["id"] for d in VEC["grayimage"]["detections"]] == [585]
+    # natural outdoor frames of the reference's game-piece data: quads, no tags
+    for name in ("frc_rebuilt_frame1", "frc_reefscape_frame6141"):
+        assert VEC[name]["detections"] == [] and VEC[name]["quads"] > 0
     assert [d["id"] for d in VEC["c1_640x480"]["detections"]] == [0, 1, 2, 554]

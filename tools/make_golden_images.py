@@ -23,7 +23,17 @@ def y_bt601(rgb: np.ndarray) -> np.ndarray:
     return y.astype(np.uint8)
 
 
-for name in ["colorimage", "colorimage_notags", "grayimage"]:
-    rgb = np.asarray(Image.open(SRC + name + ".jpg").convert("RGB"))
-    Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
-    print(name, rgb.shape)
+# real-world frames without tags from the reference's game-piece data (outdoor
+# textures: many quads, no detections) -- natural-image parity cases
+EXTRA = {"frc_rebuilt_frame1": "/root/reference/src/game_piece_detection/data/rebuilt/frame1.png",
+         "frc_reefscape_frame6141": "/root/reference/src/game_piece_detection/data/reefscape/frame_6141.jpg"}
+
+if __name__ == "__main__":
+    for name in ["colorimage", "colorimage_notags", "grayimage"]:
+        rgb = np.asarray(Image.open(SRC + name + ".jpg").convert("RGB"))
+        Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
+        print(name, rgb.shape)
+    for name, path in EXTRA.items():
+        rgb = np.asarray(Image.open(path).convert("RGB"))
+        Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
+        print(name, rgb.shape)

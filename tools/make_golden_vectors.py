@@ -28,6 +28,8 @@ def cases():
     yield "colorimage", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_y.png"))
     yield "colorimage_notags", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_notags_y.png"))
     yield "grayimage", 1280, 800, 2, np.asarray(Image.open(g + "/grayimage_y.png"))
+    yield "frc_rebuilt_frame1", 1920, 1080, 2, np.asarray(Image.open(g + "/frc_rebuilt_frame1_y.png"))
+    yield "frc_reefscape_frame6141", 640, 640, 2, np.asarray(Image.open(g + "/frc_reefscape_frame6141_y.png"))
     yield "c1_640x480", 640, 480, 0, synth.to_yuyv(synth.render_board(640, 480, seed=766, ntags=4,
                                                                        ids=[0, 1, 2, 554], codes=codes)[0])
     for f in range(3):
