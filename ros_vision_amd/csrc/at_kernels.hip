@@ -656,8 +656,10 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   // region.  Keeping the stage small keeps 6 workgroups (24 waves) per CU.
   __shared__ uint64_t s_pts[kBndStage];
   __shared__ uint32_t s_npts, s_nent;
+  // threshold values with pixels of blobs under 25 pixels folded to 127: every
+  // BlobDiff condition then reads one byte per neighbour (v0 + v1 == 255 holds
+  // only when both blobs are kept; the dedup rule's "!= 127 and kept" likewise)
   __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
-  __shared__ uint8_t s_tbig[(4 * kBndRows + 1) * 66];
   __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
   const int f = blockIdx.z;
   const int tid = threadIdx.y * 64 + threadIdx.x;
@@ -680,20 +682,20 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
   // column) -> local root -> component root (k_ccl_roots)
   uint32_t lv[kPer];
+  uint8_t tv[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
     lv[k] = 0xffffffffu;
+    tv[k] = 127;
     if (e < kTN && yy < g.Hd && xx < Wd) {
       const size_t i = (size_t)yy * Wd + xx;
       const uint32_t v = thr[i];
-      s_tthr[e] = (uint8_t)v;
+      tv[k] = (uint8_t)v;
       const uint32_t F = (uint32_t)((yy & ~1) * Wd + (xx & ~1));
       const uint32_t node = v == 255 ? F : F + Wd + (xx & 1);
       if (v != 127) lv[k] = par[node];
-    } else if (e < kTN) {
-      s_tthr[e] = 127;
     }
   }
 #pragma unroll
@@ -703,8 +705,9 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     if (e < kTN) {
+      const bool kept = lv[k] != 0xffffffffu && size[lv[k]] >= 25;
       s_tlab[e] = lv[k];
-      s_tbig[e] = lv[k] != 0xffffffffu && size[lv[k]] >= 25;
+      s_tthr[e] = kept ? tv[k] : (uint8_t)127;
     }
   }
   __syncthreads();  // LDS tables initialised
@@ -719,15 +722,15 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
     if (x <= g.Wd - 2 && y <= g.Hd - 2) {
       const int e0 = ly * kTC + threadIdx.x + 1;
       const uint8_t v0 = s_tthr[e0];
-      if (v0 != 127 && s_tbig[e0]) {
+      if (v0 != 127) {
         const uint32_t rep0 = s_tlab[e0];
         const int er = e0 + 1, ed = e0 + kTC, edr = ed + 1, edl = ed - 1, el = e0 - 1;
         const uint8_t vr = s_tthr[er], vd = s_tthr[ed], vdr = s_tthr[edr], vdl = s_tthr[edl], vl = s_tthr[el];
-        if (v0 + vr == 255 && s_tbig[er]) pk[0] = make_qbp(rep0, s_tlab[er], x, y, 0, vr > v0);
-        if (v0 + vdr == 255 && s_tbig[edr]) pk[1] = make_qbp(rep0, s_tlab[edr], x, y, 1, vdr > v0);
-        if (v0 + vd == 255 && s_tbig[ed]) pk[2] = make_qbp(rep0, s_tlab[ed], x, y, 2, vd > v0);
-        const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1 && s_tbig[el] && s_tbig[ed];
-        if (!dedup && v0 + vdl == 255 && s_tbig[edl]) pk[3] = make_qbp(rep0, s_tlab[edl], x, y, 3, vdl > v0);
+        if (v0 + vr == 255) pk[0] = make_qbp(rep0, s_tlab[er], x, y, 0, vr > v0);
+        if (v0 + vdr == 255) pk[1] = make_qbp(rep0, s_tlab[edr], x, y, 1, vdr > v0);
+        if (v0 + vd == 255) pk[2] = make_qbp(rep0, s_tlab[ed], x, y, 2, vd > v0);
+        const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1;
+        if (!dedup && v0 + vdl == 255) pk[3] = make_qbp(rep0, s_tlab[edl], x, y, 3, vdl > v0);
       }
     }
     uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
