@@ -134,37 +134,36 @@ __device__ M3 polar3(M3 x) {
   return x;
 }
 
-// U V' of a 3x3 whose third column is zero, followed by the det < 0 fix of
-// orthogonal_iteration (negate column 2): [Q | q0 x q1], Q = A (A'A)^-1/2.
-__device__ M3 polar_rank2_proper(const M3& m) {
-  const double a = m.m[0][0] * m.m[0][0] + m.m[1][0] * m.m[1][0] + m.m[2][0] * m.m[2][0];
-  const double b = m.m[0][0] * m.m[0][1] + m.m[1][0] * m.m[1][1] + m.m[2][0] * m.m[2][1];
-  const double c = m.m[0][1] * m.m[0][1] + m.m[1][1] * m.m[1][1] + m.m[2][1] * m.m[2][1];
-  // sqrt(S) = (S + d I) / tau, d = sqrt(det S), tau = sqrt(tr S + 2d);
-  // det(S + d I) = d tau^2, so (S + d I)^-1 tau = adj(S + d I) / (d tau):
-  // two reciprocal square roots, no square root and no division on the chain
+// 1/sqrt(x), x > 0: the hardware estimate and one second-order correction
+// (y (1 + e/2 + 3e^2/8), e = 1 - x y^2) -- ocml's refinement without its
+// special-case select (x = 0 and inf do not reach the callers below)
+__device__ __forceinline__ double rsqrt_pos(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double e = fma(-x * y, y, 1.0);
+  return fma(y * e, fma(0.375, e, 0.5), y);
+}
+
+// polar factor of the 3x2 block [m0 m1] (third column of M3 is zero): the
+// columns (q0, q1) of Q = A (A'A)^-1/2.  With S = A'A = [a b; b c],
+// sqrt(S) = (S + d I) / tau, d = sqrt(det S), tau = sqrt(tr S + 2d);
+// det(S + d I) = d tau^2, so (S + d I)^-1 tau = adj(S + d I) / (d tau):
+// two reciprocal square roots, no square root and no division on the chain.
+// The third column of U V' after orthogonal_iteration's det < 0 fix is q0 x q1.
+__device__ __forceinline__ void polar_rank2_cols(const V3& m0, const V3& m1, V3& q0, V3& q1) {
+  const double a = m0.v[0] * m0.v[0] + m0.v[1] * m0.v[1] + m0.v[2] * m0.v[2];
+  const double b = m0.v[0] * m1.v[0] + m0.v[1] * m1.v[1] + m0.v[2] * m1.v[2];
+  const double c = m1.v[0] * m1.v[0] + m1.v[1] * m1.v[1] + m1.v[2] * m1.v[2];
   const double D = fmax(a * c - b * b, 0.0);
-  const double rd = rsqrt(D);
+  const double rd = rsqrt_pos(D);
   const double d = D * rd;
-  const double rt = rsqrt(a + c + 2 * d);
-  const double e00 = a + d, e01 = b, e11 = c + d;
+  const double rt = rsqrt_pos(a + c + 2 * d);
   const double k = rd * rt;
-  const double i00 = e11 * k, i01 = -e01 * k, i11 = e00 * k;
-  M3 r;
-  V3 q0, q1;
+  const double i00 = (c + d) * k, i01 = -b * k, i11 = (a + d) * k;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    q0.v[i] = m.m[i][0] * i00 + m.m[i][1] * i01;
-    q1.v[i] = m.m[i][0] * i01 + m.m[i][1] * i11;
+    q0.v[i] = m0.v[i] * i00 + m1.v[i] * i01;
+    q1.v[i] = m0.v[i] * i01 + m1.v[i] * i11;
   }
-  const V3 q2 = v_cross(q0, q1);
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    r.m[i][0] = q0.v[i];
-    r.m[i][1] = q1.v[i];
-    r.m[i][2] = q2.v[i];
-  }
-  return r;
 }
 
 __device__ __forceinline__ M3 calculate_F(const V3& v) {
@@ -185,9 +184,7 @@ __device__ __forceinline__ M3 calculate_F(const V3& v) {
 //   M3[:,0] = (s^2 F_s + G_x T_x) r0 + (F_xy + G_x T_y) r1
 //   M3[:,1] = (F_xy + G_y T_x) r0 + (s^2 F_s + G_y T_y) r1
 // (sum_j sx_j = sum_j sy_j = 0 removes the I and q_mean terms).  The step is
-// then R <- polar(M3); it is deterministic, so once an iterate repeats
-// (fixed point or 2-cycle) the remaining steps are known exactly and the loop
-// stops.  As upstream, the returned t belongs to the R before the last step
+// then R <- polar(M3).  As upstream, the returned t belongs to the R before the last step
 // and the error to the final (R, t).
 __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, int n_steps, int* steps = nullptr) {
   M3 F[4];
@@ -237,56 +234,42 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
       A10.m[i][j] = Fxy.m[i][j] + GyTx.m[i][j];
       A11.m[i][j] = s2 * Fs.m[i][j] + GyTy.m[i][j];
     }
-  // iterate on (r0, r1)
+  // iterate on (r0, r1).  The step contracts slowly (rate ~0.9 for typical
+  // tag geometry, so the iterate still moves ~1e-5..1e-4 at step 50): all
+  // n_steps run, with no per-step exit test; (q0, q1) keeps iterate k - 1,
+  // whose t upstream returns
   V3 r0 = {{R->m[0][0], R->m[1][0], R->m[2][0]}}, r1 = {{R->m[0][1], R->m[1][1], R->m[2][1]}};
-  V3 q0 = r0, q1 = r1;      // iterate k-1
-  V3 w0 = r0, w1 = r1;      // iterate k-2
-  M3 Rn = *R;
-  int k = 0;
-  bool cyc2 = false;
-  for (k = 1; k <= n_steps; k++) {
-    M3 M;
+  V3 q0 = r0, q1 = r1;
+  auto step = [&](const V3& x0, const V3& x1, V3& y0, V3& y1) {
     V3 m0, m1;
 #pragma unroll
     for (int i = 0; i < 3; i++) {  // balanced 6-term dot products
-      m0.v[i] = ((A00.m[i][0] * r0.v[0] + A00.m[i][1] * r0.v[1]) + (A00.m[i][2] * r0.v[2] + A01.m[i][0] * r1.v[0])) +
-                (A01.m[i][1] * r1.v[1] + A01.m[i][2] * r1.v[2]);
-      m1.v[i] = ((A10.m[i][0] * r0.v[0] + A10.m[i][1] * r0.v[1]) + (A10.m[i][2] * r0.v[2] + A11.m[i][0] * r1.v[0])) +
-                (A11.m[i][1] * r1.v[1] + A11.m[i][2] * r1.v[2]);
+      m0.v[i] = ((A00.m[i][0] * x0.v[0] + A00.m[i][1] * x0.v[1]) + (A00.m[i][2] * x0.v[2] + A01.m[i][0] * x1.v[0])) +
+                (A01.m[i][1] * x1.v[1] + A01.m[i][2] * x1.v[2]);
+      m1.v[i] = ((A10.m[i][0] * x0.v[0] + A10.m[i][1] * x0.v[1]) + (A10.m[i][2] * x0.v[2] + A11.m[i][0] * x1.v[0])) +
+                (A11.m[i][1] * x1.v[1] + A11.m[i][2] * x1.v[2]);
     }
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      M.m[i][0] = m0.v[i];
-      M.m[i][1] = m1.v[i];
-      M.m[i][2] = 0;
-    }
-    Rn = polar_rank2_proper(M);
-    w0 = q0; w1 = q1;
-    q0 = r0; q1 = r1;
-    r0 = V3{{Rn.m[0][0], Rn.m[1][0], Rn.m[2][0]}};
-    r1 = V3{{Rn.m[0][1], Rn.m[1][1], Rn.m[2][1]}};
-    bool same1 = true, same2 = k >= 2;
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-      same1 = same1 && r0.v[i] == q0.v[i] && r1.v[i] == q1.v[i];
-      same2 = same2 && r0.v[i] == w0.v[i] && r1.v[i] == w1.v[i];
-    }
-    if (same1) break;                // fixed point: every later iterate equals it
-    if (same2) { cyc2 = true; break; }  // 2-cycle: iterates alternate
+    polar_rank2_cols(m0, m1, y0, y1);
+  };
+  int k = 0;
+  for (; k + 2 <= n_steps; k += 2) {  // two steps per trip: no register rotation
+    step(r0, r1, q0, q1);
+    step(q0, q1, r0, r1);
   }
-  if (steps) *steps = k;
-  // state after n_steps: (r0, r1) = iterate n_steps, (q0, q1) = iterate n_steps - 1
-  if (k <= n_steps && cyc2 && ((n_steps - k) & 1)) {
+  if (k < n_steps) {  // odd n_steps
+    step(r0, r1, q0, q1);
     const V3 a0 = r0, a1 = r1;
     r0 = q0; r1 = q1;
     q0 = a0; q1 = a1;
-    const V3 r2 = v_cross(r0, r1);
+  }
+  if (steps) *steps = n_steps + 1;
+  M3 Rn;
+  const V3 r2 = v_cross(r0, r1);
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
-      Rn.m[i][0] = r0.v[i];
-      Rn.m[i][1] = r1.v[i];
-      Rn.m[i][2] = r2.v[i];
-    }
+  for (int i = 0; i < 3; i++) {
+    Rn.m[i][0] = r0.v[i];
+    Rn.m[i][1] = r1.v[i];
+    Rn.m[i][2] = r2.v[i];
   }
   *R = Rn;
   *t = v_add(mv(Tx, q0), mv(Ty, q1));
