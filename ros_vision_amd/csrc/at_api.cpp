@@ -202,7 +202,10 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.BTX = (g.Wd - 2 + 63) / 64;
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
   g.ntb = g.BTX * g.BTY;
-  if (g.ntb > kMaxTilesPerFrame) return AT_E_INVALID;
+  if (g.ntb > kMaxTilesPerFrame) {
+    at_destroy(d);
+    return AT_E_INVALID;
+  }
   g.min_cluster = (uint32_t)std::max(24, cfg->min_cluster_pixels);
   g.max_cluster = (uint32_t)(2 * (W + H));
   g.min_tag_width = std::max(3, 8 / 2);  // tag36h11 width_at_border 8 / quad_decimate 2
@@ -219,7 +222,10 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
   p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
-  if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) return AT_E_INVALID;
+  if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {
+    at_destroy(d);
+    return AT_E_INVALID;
+  }
   p.tag_size = cfg->tag_size;
 
   auto fail = [&](int code) {
@@ -562,7 +568,7 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
     const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
     const int ncand = (int)std::min<uint32_t>(d->h_ctrl[kCtlNdets * B + f], (uint32_t)kMaxDets);
     int n = 0;
-    if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow)) {
+    if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow)) {
       rc = AT_E_CAPACITY;
     } else {
       n = host_tail(d->h_dets + (size_t)f * kMaxDets, ncand, out ? out + (size_t)f * cap_per_frame : nullptr,
@@ -720,7 +726,7 @@ int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const d
 int at_frame_status(at_detector* d, int frame) {
   if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
   const uint32_t s = d->h_ctrl[kCtlStatus * d->B + frame];
-  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow))
+  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow))
              ? AT_E_CAPACITY
              : AT_OK;
 }

@@ -22,7 +22,6 @@ constexpr int kBndStage = 1536;                 // of which staged in LDS (1.5 p
 constexpr int kLdsPairSlots = 512;
 constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
-constexpr int kMaxDets = 128;          // candidate detections per frame
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
 // Blobs of more than kSmallBlob points: one workgroup each, 512 threads for
@@ -51,7 +50,12 @@ constexpr uint32_t kStatusDetsOverflow = 4u;
 constexpr uint32_t kStatusPointsOverflow = 8u;
 constexpr uint32_t kStatusQuadsOverflow = 16u;
 constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config.max_batch)
-constexpr int kQuadCandPerFrame = 512;  // accepted quads queued for decode, per frame of the batch
+// Every kept blob pair can yield one accepted quad and every accepted quad at most
+// one detection, so sizing both queues by kMaxPairs makes neither of them a cap:
+// the reference decodes every quad (apriltag_detect.cu:618-663).
+constexpr int kQuadCandPerFrame = kMaxPairs;  // accepted quads queued for decode, per frame
+constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections per frame (before reconcile)
+constexpr int kMaxCodes = 1024;               // codebook entries (tag36h11: 587)
 
 // Frame geometry (all derived from W, H).
 struct Geom {

@@ -143,8 +143,8 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 
 struct DevCodebook {
   int n;
-  uint64_t code[96];
-  int id[96];
+  uint64_t code[kMaxCodes];
+  int id[kMaxCodes];
 };
 __constant__ DevCodebook c_book;
 
@@ -2881,15 +2881,20 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     __syncthreads();
     phase(8);
     // quick_decode_codeword: first rotation, then entry, within hamming <= 2
+    // (codes are >= 11 apart, so at most one entry matches a rotation)
     uint32_t bc = 0xffffffffu;
     {
-      const uint64_t rcode = S.rcode;
-      for (int t = tid; t < 4 * c_book.n; t += kDecodeThreads) {
-        const int rot = t / c_book.n, ent = t % c_book.n;
-        uint64_t r = rcode;
-        for (int k = 0; k < rot; k++) r = rotate90_36(r);
-        const int hd = __popcll(r ^ c_book.code[ent]);
-        if (hd <= 2) bc = min(bc, (uint32_t)((rot << 24) | (hd << 16) | ent));
+      uint64_t r[4];
+      r[0] = S.rcode;
+#pragma unroll
+      for (int k = 1; k < 4; k++) r[k] = rotate90_36(r[k - 1]);
+      for (int ent = tid; ent < c_book.n; ent += kDecodeThreads) {
+        const uint64_t c = c_book.code[ent];
+#pragma unroll
+        for (int rot = 0; rot < 4; rot++) {
+          const int hd = __popcll(r[rot] ^ c);
+          if (hd <= 2) bc = min(bc, (uint32_t)((rot << 24) | (hd << 16) | ent));
+        }
       }
 #pragma unroll
       for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
@@ -2936,7 +2941,8 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
 hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
   DevCodebook cb;
   cb.n = n;
-  for (int i = 0; i < n && i < 96; i++) {
+  if (n < 0 || n > kMaxCodes) return hipErrorInvalidValue;
+  for (int i = 0; i < n; i++) {
     cb.code[i] = codes[i];
     cb.id[i] = ids[i];
   }
@@ -2952,28 +2958,30 @@ hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
 // One detection per quad of lanes (16 per wave): the four lanes compute the
 // same pose, splitting only the quartic's root brackets; lane 0 of the quad stores.
 constexpr int kPoseLanes = 4;
+constexpr int kPoseGroupsPerFrame = 8;  // 128 detections per pass, looped beyond
 __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
   const int f = blockIdx.y;
-  const uint32_t i = blockIdx.x * (64 / kPoseLanes) + threadIdx.x / kPoseLanes;
   const int sub = (int)(threadIdx.x % kPoseLanes);
   // the control block is final once k_decode has finished: block (0, 0) hands it
   // to the host (replaces a device-to-host copy)
   if (blockIdx.x == 0 && blockIdx.y == 0)
     for (uint32_t w = threadIdx.x; w < b.ctrl_words; w += 64) b.hctrl[w] = b.ctrl[w];
   const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
-  if (i >= n) return;  // uniform across the quad
-  DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
-  double R[9], t[3], err[2];
-  pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
-                          (prm.probe && f == 0 && i == 0 && sub == 0) ? b.probe + 16 : nullptr);
-  if (sub == 0) {
-    DevDetection& h = b.hdets[(size_t)f * kMaxDets + i];
+  for (uint32_t i = blockIdx.x * (64 / kPoseLanes) + threadIdx.x / kPoseLanes; i < n;  // uniform across the quad
+       i += gridDim.x * (64 / kPoseLanes)) {
+    DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
+    double R[9], t[3], err[2];
+    pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
+                            (prm.probe && f == 0 && i == 0 && sub == 0) ? b.probe + 16 : nullptr);
+    if (sub == 0) {
+      DevDetection& h = b.hdets[(size_t)f * kMaxDets + i];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
+      for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
 #pragma unroll
-    for (int k = 0; k < 3; k++) d.pose_t[k] = h.pose_t[k] = t[k];
-    d.pose_err[0] = h.pose_err[0] = err[0];
-    d.pose_err[1] = h.pose_err[1] = err[1];
+      for (int k = 0; k < 3; k++) d.pose_t[k] = h.pose_t[k] = t[k];
+      d.pose_err[0] = h.pose_err[0] = err[0];
+      d.pose_err[1] = h.pose_err[1] = err[1];
+    }
   }
 }
 
@@ -3090,7 +3098,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   mark();
   tk(11, st, 0);
   if (prm.tag_size > 0)
-    hipLaunchKernelGGL(k_pose, dim3((kMaxDets * kPoseLanes + 63) / 64, B), dim3(64), 0, st, b, prm);
+    hipLaunchKernelGGL(k_pose, dim3(kPoseGroupsPerFrame, B), dim3(64), 0, st, b, prm);
   tk(11, st, 1);
   mark();
   if (split_err != hipSuccess) return split_err;

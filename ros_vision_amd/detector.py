@@ -224,7 +224,7 @@ def _check(rc, what):
 class GpuDetector:
     """Drop-in for frc971::apriltag::GpuDetector on MI355X (one instance per camera)."""
 
-    MAX_DETECTIONS = 128
+    MAX_DETECTIONS = 1024  # per frame returned to Python (the library keeps up to 4096 per frame)
 
     def __init__(self, width, height, camera_matrix: CameraMatrix = TEST_CAMERA,
                  distortion_coefficients: DistCoeffs = TEST_DIST, family="tag36h11",

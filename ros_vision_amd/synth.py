@@ -6,8 +6,9 @@ grid; each tag gets a random side length, rotation and perspective
 bitmap (white quiet zone, black border, 6x6 data cells in the apriltag 3.x
 bit layout) and the frame gets Gaussian noise.  Output is the gray plane or
 packed YUYV with U = V = 128 (what cvtColor(BGR2YUV_YUYV) produces for a gray
-image, apriltags_cuda_detector.cu:401).  Only ids whose codeword is known
-offline are used (codebook).
+image, apriltags_cuda_detector.cu:401).  Stream frames (configs C2-C4) carry
+ids 10f .. 10f+ntags-1 mod 587, so a run of frames walks
+the whole tag36h11 family.
 """
 import numpy as np
 
@@ -106,6 +107,22 @@ def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigm
     return gray, truth
 
 
+def render_dots(width: int, height: int, seed: int, side: int = 20, pitch: int = 40, noise_sigma: float = 2.0):
+    """Dark squares on a light background on a jittered grid: every square is a
+    blob pair that fits a quad (more accepted quads than tags fit in a frame)."""
+    rng = np.random.default_rng(seed)
+    img = np.full((height, width), 220.0, np.float32)
+    n = 0
+    for y in range(pitch // 2, height - pitch // 2 - side, pitch):
+        for x in range(pitch // 2, width - pitch // 2 - side, pitch):
+            jx, jy = rng.integers(-pitch // 6, pitch // 6 + 1, size=2)
+            img[y + jy:y + jy + side, x + jx:x + jx + side] = 30.0
+            n += 1
+    if noise_sigma > 0:
+        img += rng.normal(0.0, noise_sigma, size=img.shape).astype(np.float32)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8), n
+
+
 def to_yuyv(gray: np.ndarray) -> np.ndarray:
     """Pack a gray plane as YUYV 4:2:2 (Y0 U Y1 V) with U = V = 128."""
     h, w = gray.shape
@@ -115,7 +132,14 @@ def to_yuyv(gray: np.ndarray) -> np.ndarray:
     return out
 
 
+def stream_ids(frame: int, ntags: int = 15, nfamily: int = 587):
+    """Config C2 ids of one frame: 10f .. 10f+ntags-1 mod 587, unique per frame."""
+    return [(10 * frame + j) % nfamily for j in range(ntags)]
+
+
 def stream_frame(width: int, height: int, frame: int, camera: int = 0, ntags: int = 15, codes=None):
-    """Config C2/C3 frame: seed 766000 + frame (+ camera * 10**6)."""
-    gray, truth = render_board(width, height, seed=766000 + frame + camera * 10 ** 6, ntags=ntags, codes=codes)
+    """Config C2/C3 frame: seed 766000 + frame (+ camera * 10**6), ids stream_ids(frame)."""
+    codes = codes if codes is not None else _codes()
+    gray, truth = render_board(width, height, seed=766000 + frame + camera * 10 ** 6, ntags=ntags,
+                               ids=stream_ids(frame, ntags, len(codes)), codes=codes)
     return to_yuyv(gray), gray, truth

@@ -1,26 +1,53 @@
 """tag36h11 codebook checks (CPU).
 
 The 587 codewords are third-party data (cgpadwick/apriltag@3.3.0 tag36h11.c,
-fetched by src/external/CMakeLists.txt:86-95, not vendored).  The pinned entries
-are checked here arithmetically, without the upstream file:
-  * ids 0..72, mapped to the 2.x row-major layout, lie on the generator
-    progression v0 + k * 982451653 (mod 2^36), v0 = Java Random(361110).nextLong(),
-    with k strictly increasing in id order;
-  * ids 554 / 585 are the codes read from the reference's fixture photographs
-    (tools/read_fixture_codes.py) and are found by the detector on those images
-    (tests/test_oracle.py, tests/test_gpu_parity.py);
-  * every pair of pinned codes keeps Hamming distance >= 11 over the four
-    rotations (the family's minimum distance), and no code is within 11 of its
-    own rotations;
+fetched by src/external/CMakeLists.txt:86-95, not vendored; used through
+tag36h11_create() at src/apriltags_cuda/src/apriltag_utils.cu:12).  The table is
+regenerated offline by tools/tag36h11_gen.c (AprilTag lexicode search) and is
+pinned here without the upstream file:
+  * ids 0..72 equal the codes recalled from tag36h11.c (RECALLED below);
+  * ids 554 / 585 equal the codes read from the reference's fixture photographs
+    (tools/read_fixture_codes.py; the detector finds them on those images,
+    tests/test_oracle.py, tests/test_gpu_parity.py), and the search reaches them
+    at k = 6235272729 and 42477048845 of the progression;
+  * every code, mapped to the 2.x row-major layout, lies on the generator
+    progression v0 + k * 982451653 (mod 2^36) with k strictly increasing in id order;
+  * every pair of codes keeps Hamming distance >= 11 over the four rotations and
+    every code has greedy rectangle complexity >= 10;
+  * the generator itself, run over k <= 2*10^6, reproduces the table's prefix;
   * the product library and the oracle carry the same table.
 """
+import shutil
+import subprocess
+from pathlib import Path
+
 import pytest
 
+ROOT = Path(__file__).resolve().parents[1]
 M36 = (1 << 36) - 1
 PRIME = 982451653
 # apriltag 3.x tag36h11 bit_x / bit_y (bit i is code bit 35 - i)
 BX = [1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3]
 BY = [1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4]
+
+# ids 0..72 as recalled from upstream tag36h11.c (3.x bit order)
+RECALLED = [
+    0xd7e00984b, 0xdda664ca7, 0xdc4a1c821, 0xe17b470e9, 0xef91d01b1, 0xf429cdd73,
+    0x05da29225, 0x1106cba43, 0x223bed79d, 0x21f51213c, 0x33eb19ca6, 0x3f76eb0f8,
+    0x469a97414, 0x45dcfe0b0, 0x4a6465f72, 0x51801db96, 0x5eb946b4e, 0x68a7cc2ec,
+    0x6f0ba2652, 0x78765559d, 0x87b83d129, 0x86cc4a5c5, 0x8b64df90f, 0x9c577b611,
+    0xa3810f2f5, 0xaf4d75b83, 0xb59a03fef, 0xbb1096f85, 0xd1b92fc76, 0xd0dd509d2,
+    0xe2cfda160, 0x2ff497c63, 0x47240671b, 0x5047a2e55, 0x635ca87c7, 0x691254166,
+    0x68f43d94a, 0x6ef24bdb6, 0x8cdd8f886, 0x9de96b718, 0xaff6e5a8a, 0xbae46f029,
+    0xd225b6d59, 0xdf8ba8c01, 0xe3744a22f, 0xfbb59375d, 0x18a916828, 0x22f29c1ba,
+    0x286887d58, 0x41392322e, 0x75d18ecd1, 0x87c302743, 0x8c6317ba9, 0x9e40f36d7,
+    0xc0e5a806a, 0xcc78cb87c, 0x12d2f2d01, 0x379f36a21, 0x6973f59ac, 0x7789ea9f4,
+    0x8f1c73e84, 0x8dd287a20, 0x94a4eee4c, 0xa455379b5, 0xa9e92987d, 0xbd25cb40b,
+    0xbe98d3582, 0xd3d5972b2, 0x14c53d7c7, 0x4f1796936, 0x4e71fed1a, 0x66d46fae0,
+    0xa55abb933,
+]
+# read from the reference's fixture photographs (tools/read_fixture_codes.py)
+FIXTURE = {554: 0xea3a7a180, 585: 0x2164f73a0}
 
 
 def java_next_long(seed):
@@ -57,6 +84,40 @@ def rot90(v):
     return out
 
 
+def _rects():
+    out = []
+    for y1 in range(6):
+        for y0 in range(y1 + 1):
+            for x0 in range(6):
+                for x1 in range(x0, 6):
+                    m = 0
+                    for y in range(y0, y1 + 1):
+                        for x in range(x0, x1 + 1):
+                            m |= 1 << (35 - (y * 6 + x))
+                    out.append(m)
+    return out
+
+
+def complexity(t, cap=10):
+    """Greedy rectangle painting count from an unpainted grid (tools/tag36h11_gen.c)."""
+    rects = _rects()
+    tb = M36 & ~t
+    w = b = 0
+    n = 0
+    while not (w == t and b == tb):
+        best = -1
+        for m in rects:
+            for nw, nb in ((w | m, b & ~m), (w & ~m, b | m)):
+                s = bin(nw & t).count("1") + bin(nb & tb).count("1")
+                if s >= best:
+                    best, bw, bb = s, nw, nb
+        w, b = bw, bb
+        n += 1
+        if n >= cap:
+            break
+    return n
+
+
 @pytest.fixture(scope="module")
 def entries(oracle_mod):
     return oracle_mod.family_entries()
@@ -65,18 +126,23 @@ def entries(oracle_mod):
 def test_product_and_oracle_tables_match(entries):
     import ros_vision_amd as rva
     assert rva.family_entries() == entries
-    assert [i for i, _ in entries] == list(range(73)) + [554, 585]
+    assert [i for i, _ in entries] == list(range(587))
+
+
+def test_pinned_entries(entries):
+    codes = dict(entries)
+    assert [codes[i] for i in range(73)] == RECALLED
+    for i, c in FIXTURE.items():
+        assert codes[i] == c, i
 
 
 def test_generator_progression(entries):
     v0 = java_next_long(361110) & M36
     assert v0 == 0xCE84479FA
     inv = pow(PRIME, -1, 1 << 36)
-    ks = [((to_row_major(c) - v0) * inv) & M36 for i, c in entries]
-    head = ks[:73]
-    assert head == sorted(head) and len(set(head)) == 73 and head[0] == 2 and head[-1] == 409
-    # the fixture codes lie far along the same progression, in id order
-    assert ks[73] == 6235272729 and ks[74] == 42477048845
+    ks = [((to_row_major(c) - v0) * inv) & M36 for _, c in entries]
+    assert ks == sorted(ks) and len(set(ks)) == 587 and ks[0] == 2 and ks[72] == 409
+    assert ks[554] == 6235272729 and ks[585] == 42477048845
 
 
 def test_minimum_hamming_distance(entries):
@@ -89,5 +155,27 @@ def test_minimum_hamming_distance(entries):
         rots.append(r)
         assert min(bin(v ^ r[j]).count("1") for j in (1, 2, 3)) >= 11
     for a in range(len(vs)):
+        va = vs[a]
         for b in range(a + 1, len(vs)):
-            assert min(bin(vs[a] ^ rb).count("1") for rb in rots[b]) >= 11, (entries[a][0], entries[b][0])
+            for rb in rots[b]:
+                assert bin(va ^ rb).count("1") >= 11, (a, b)
+
+
+def test_complexity_of_sampled_codes(entries):
+    vs = [to_row_major(c) for _, c in entries]
+    for i in list(range(0, 587, 37)) + [554, 585, 586]:
+        assert complexity(vs[i]) >= 10, i
+    # rejected candidates: k = 1 and 5 pass every Hamming test but are too simple
+    v0 = java_next_long(361110) & M36
+    assert complexity((v0 + PRIME) & M36) < 10
+    assert complexity((v0 + 5 * PRIME) & M36) < 10
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_generator_reproduces_prefix(entries, tmp_path):
+    exe = tmp_path / "gen"
+    subprocess.run(["gcc", "-O2", "-fopenmp", str(ROOT / "tools/tag36h11_gen.c"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "2000000"], check=True, capture_output=True, text=True).stdout
+    got = [(int(l.split()[0]), int(l.split()[3], 16)) for l in out.splitlines()]
+    assert len(got) > 200
+    assert got == entries[:len(got)]

@@ -32,10 +32,16 @@ def cases():
     yield "frc_reefscape_frame6141", 640, 640, 2, np.asarray(Image.open(g + "/frc_reefscape_frame6141_y.png"))
     yield "c1_640x480", 640, 480, 0, synth.to_yuyv(synth.render_board(640, 480, seed=766, ntags=4,
                                                                        ids=[0, 1, 2, 554], codes=codes)[0])
-    for f in range(3):
+    for f in (0, 1, 2, 30, 44, 58):  # ids 10f..10f+14 mod 587 across the family
         yield "c2_720p_f%d" % f, 1280, 720, 0, synth.stream_frame(1280, 720, f, codes=codes)[0]
     yield "c4_1080p", 1920, 1080, 0, synth.to_yuyv(synth.render_board(1920, 1080, seed=4242, ntags=24,
                                                                        codes=codes)[0])
+    # more tags than the former 128-detection cap, ids 400.. across the wrap to 0..
+    yield "dense_1080p_160tags", 1920, 1080, 0, synth.to_yuyv(synth.render_board(
+        1920, 1080, seed=9160, ntags=160, side_range=(50, 64), ids=[(400 + j) % 587 for j in range(160)],
+        codes=codes)[0])
+    # more accepted quads than the former 512-quad decode queue
+    yield "dots_1080p", 1920, 1080, 2, synth.render_dots(1920, 1080, seed=9512)[0]
 
 
 def digest(a):
