@@ -85,6 +85,7 @@ def lib():
                                            D, D, D]
         L.ao_rotate90.argtypes = [C.c_uint64]
         L.ao_unrank.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
+        L.ao_set_fp_perturb.argtypes = [C.c_int]
         _LIB = L
     return _LIB
 
@@ -197,6 +198,12 @@ def estimate_tag_pose(H, corners, fx, fy, cx, cy, tagsize=0.1651):
                                      R.ctypes.data_as(D), t.ctypes.data_as(D), e.ctypes.data_as(D))
     err = e[0] if e[0] <= e[1] else e[1]
     return R.reshape(3, 3), t, err, (e[0], e[1]), bool(sec)
+
+
+def set_fp_perturb(mask: int):
+    """Sensitivity hook: bit k (0 atan2f, 1 hypotf, 2 cosf, 3 sinf) moves every result of
+    that function 1 ulp (bit 8: towards -inf).  0 restores the exact restatement."""
+    lib().ao_set_fp_perturb(int(mask))
 
 
 def family_entries():

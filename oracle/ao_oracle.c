@@ -67,7 +67,23 @@ static double det_atan2(double y, double x) {
   return a;
 }
 
-float ao_det_atan2f(float y, float x) { return (float)det_atan2((double)y, (double)x); }
+/* Sensitivity hook (tools/fp_sensitivity.py, tests only): bit k of ao_fp_perturb
+ * (0 atan2f, 1 hypotf, 2 cosf, 3 sinf) moves the results of that function one
+ * ulp, towards -inf when bit 8 is set, else towards +inf; with bit 9 set, results
+ * that are exact (a faithful libm returns them unchanged: hypotf of a Pythagorean
+ * pair, atan2f(0, x > 0), sinf(0), cosf(0)) are left alone.  0 = exact restatement. */
+static int ao_fp_perturb = 0;
+void ao_set_fp_perturb(int mask) { ao_fp_perturb = mask; }
+static float fp_perturb(float v, int bit, int exact) {
+  if (!(ao_fp_perturb & (1 << bit))) return v;
+  if (exact && (ao_fp_perturb & 512)) return v;
+  return nextafterf(v, (ao_fp_perturb & 256) ? -INFINITY : INFINITY);
+}
+
+float ao_det_atan2f(float y, float x) {
+  return fp_perturb((float)det_atan2((double)y, (double)x), 0, y == 0.0f && x > 0.0f);
+}
+
 
 static const double kSinC[6] = {1.58962301576546568060E-10, -2.50507477628578072866E-8,
                                 2.75573136213857245213E-6,  -1.98412698295895385996E-4,
@@ -100,11 +116,12 @@ static void det_sincos(double x, double *s, double *c) {
     default: *s = -cr; *c = sr; break;
   }
 }
-float ao_det_cosf(float x) { double s, c; det_sincos((double)x, &s, &c); return (float)c; }
-float ao_det_sinf(float x) { double s, c; det_sincos((double)x, &s, &c); return (float)s; }
+float ao_det_cosf(float x) { double s, c; det_sincos((double)x, &s, &c); return fp_perturb((float)c, 2, x == 0.0f); }
+float ao_det_sinf(float x) { double s, c; det_sincos((double)x, &s, &c); return fp_perturb((float)s, 3, x == 0.0f); }
 float ao_det_hypotf(float a, float b) {
   double x = a, y = b;
-  return (float)sqrt(x * x + y * y);
+  const double d = x * x + y * y, r = sqrt(d);
+  return fp_perturb((float)r, 1, r == (double)(float)r && r * r == d);
 }
 #define det_atan2f ao_det_atan2f
 #define det_cosf ao_det_cosf

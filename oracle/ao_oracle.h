@@ -120,6 +120,8 @@ int ao_estimate_tag_pose(const double H[9], const double corners[4][2], double f
 /* helpers exposed for tests */
 uint64_t ao_rotate90(uint64_t w);
 int ao_unrank(int i, int *m0, int *m1, int *m2, int *m3);
+/* ulp-sensitivity hook (tests only): see ao_oracle.c */
+void ao_set_fp_perturb(int mask);
 
 #ifdef __cplusplus
 }

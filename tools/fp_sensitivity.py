@@ -1,0 +1,110 @@
+"""How far is "bit-exact vs the oracle" from "bit-exact vs the reference"?
+
+The oracle and the HIP kernels replace libm's atan2f / hypotf / cosf / sinf by
+one fixed sequence (ros_vision_amd/csrc/at_detmath.h, within 1 ulp of glibc).
+The reference computes them with CUDA's libdevice on the Orin, which can differ
+by an ulp.  These functions feed integer decisions: theta keys
+(llrintf(...*8e6), apriltag_gpu.cu:402-404), line-fit weights W
+((int)(hypotf+1), apriltag_gpu.cu:656), FitLineError (line_fit_filter.cu:33)
+and so the peak and quad-argmin decisions.
+
+This tool moves every result of one function by one ulp (up, then down; then
+all four together) through the oracle's ao_set_fp_perturb hook and counts, per
+golden case, what flips against the exact restatement:
+  theta_keys     index points whose 64-bit key changed (theta value or order)
+  theta_order    index points whose position in the sorted (blob, theta) stream changed
+  fitquad_moments FitQuad records whose integer moments changed (W)
+  peaks          change in the number of line-fit peaks
+  quad_indices   FitQuad records whose 4 corner indices or valid flag changed
+  quads          accepted quads added, removed or moved by > 1e-3 px
+  detections     detections whose id set changed or corners moved > 1e-4 px
+  det_corner_max_px / det_integer_corner_changes   largest corner move, corners whose integer part moved
+
+usage: python tools/fp_sensitivity.py [--write]   (writes tests/golden/fp_sensitivity.json)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import ao  # noqa: E402
+
+FUNCS = {"atan2f": 1, "hypotf": 2, "cosf": 4, "sinf": 8}
+CONFIGS = [(n + d, m | (256 if d == "-" else 0)) for n, m in FUNCS.items() for d in ("+", "-")]
+CONFIGS += [("all+", 15), ("all-", 15 | 256)]
+# faithful-libm model: inexact results move one ulp, exact ones (hypotf of a Pythagorean pair, ...) do not
+CONFIGS += [(n + d + "_inexact", m | 512 | (256 if d == "-" else 0)) for n, m in FUNCS.items() for d in ("+", "-")]
+CONFIGS += [("all+_inexact", 15 | 512), ("all-_inexact", 15 | 256 | 512)]
+
+
+def snapshot(W, H, fmt, frame):
+    o = ao.Oracle(W, H)
+    o.detect(frame, fmt)
+    fq = o.fitquads()
+    return {
+        "ip": o.sorted_index_points(),
+        "mom": [(tuple(f.Mx), tuple(f.My), tuple(f.W), tuple(f.Mxx), tuple(f.Myy), tuple(f.Mxy)) for f in fq],
+        "idx": [(int(f.blob_index), tuple(f.indices), int(f.valid)) for f in fq],
+        "peaks": o.num_peaks(),
+        "quads": {b: c for c, b in o.quads()},
+        "dets": {d["id"]: d["p"] for d in o.detections()},
+    }
+
+
+def diff(a, b):
+    n = min(a["ip"].size, b["ip"].size)
+    theta = int(np.count_nonzero(a["ip"][:n] != b["ip"][:n])) + abs(a["ip"].size - b["ip"].size)
+    # order of the sorted stream: blob [63:52] and point bits [23:0], theta masked out
+    m = np.uint64(0xFFF0000000FFFFFF)
+    order = int(np.count_nonzero((a["ip"][:n] & m) != (b["ip"][:n] & m))) + abs(a["ip"].size - b["ip"].size)
+    mom = sum(x != y for x, y in zip(a["mom"], b["mom"])) + abs(len(a["mom"]) - len(b["mom"]))
+    idx = sum(x != y for x, y in zip(a["idx"], b["idx"])) + abs(len(a["idx"]) - len(b["idx"]))
+    qa, qb = a["quads"], b["quads"]
+    quads = len(set(qa) ^ set(qb)) + sum(float(np.abs(qa[k] - qb[k]).max()) > 1e-3 for k in set(qa) & set(qb))
+    da, db = a["dets"], b["dets"]
+    dets = len(set(da) ^ set(db)) + sum(float(np.abs(da[k] - db[k]).max()) > 1e-4 for k in set(da) & set(db))
+    common = set(da) & set(db)
+    dmax = max([float(np.abs(da[k] - db[k]).max()) for k in common] or [0.0])
+    dfloor = sum(not np.array_equal(np.floor(da[k]), np.floor(db[k])) for k in common)
+    return {"theta_keys": theta, "theta_order": order, "fitquad_moments": mom, "peaks": abs(a["peaks"] - b["peaks"]),
+            "quad_indices": idx, "quads": quads, "detections": dets,
+            "det_corner_max_px": dmax, "det_integer_corner_changes": dfloor}
+
+
+def run():
+    import make_golden_vectors as mg
+    res = {}
+    for name, W, H, fmt, frame in mg.cases():
+        ao.set_fp_perturb(0)
+        base = snapshot(W, H, fmt, frame)
+        res[name] = {"index_points": int(base["ip"].size), "fitquads": len(base["idx"]),
+                     "quads": len(base["quads"]), "detections": len(base["dets"])}
+        for cname, mask in CONFIGS:
+            ao.set_fp_perturb(mask)
+            res[name][cname] = diff(base, snapshot(W, H, fmt, frame))
+        ao.set_fp_perturb(0)
+    return res
+
+
+def totals(res):
+    out = {}
+    for cname, _ in CONFIGS:
+        out[cname] = {k: (max if k == "det_corner_max_px" else sum)(r[cname][k] for r in res.values())
+                      for k in next(iter(res.values()))[cname]}
+    out["index_points"] = sum(r["index_points"] for r in res.values())
+    out["fitquads"] = sum(r["fitquads"] for r in res.values())
+    out["detections"] = sum(r["detections"] for r in res.values())
+    return out
+
+
+if __name__ == "__main__":
+    res = run()
+    doc = {"cases": res, "totals": totals(res)}
+    print(json.dumps(doc["totals"], indent=1))
+    if "--write" in sys.argv:
+        json.dump(doc, open(os.path.join(ROOT, "tests", "golden", "fp_sensitivity.json"), "w"), indent=1)

@@ -1,25 +1,38 @@
 #!/bin/bash
-# One GPU call: rocprofv3 kernel-trace stats of the bench command, then two
-# separate PMC passes (FETCH_SIZE, WRITE_SIZE; never combined with traces),
-# then the plain bench line.  Output: gpurun_out/$TAG/...
-# usage: bash tools/profile_round.sh TAG
+# One GPU call collecting this round's profiles (MI355X_MICROARCH.md HBM/rocprofv3):
+#   1. rocprofv3 --kernel-trace --stats of the default bench (timed-region config)
+#   2. FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass (never with traces)
+#   3. two SQ counter passes (8 SQ counters each)
+#   4. FETCH_SIZE / WRITE_SIZE passes over tools/pmc_calib (known byte counts per
+#      access width, for the gfx950 correction)
+#   5. the plain bench line
+# Output: gpurun_out/$TAG/...   usage: bash tools/profile_round.sh TAG [BATCH]
 set -euo pipefail
 TAG=${1:-prof}
+BATCH=${2:-32}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --no-cpu-baseline --steps 20 --warmup 3 --latency-frames 20"
+SHORT="$ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 4 --warmup 1 --latency-frames 0"
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --steps 4 --warmup 1 --latency-frames 0 > /dev/null 2> "$OUT/pmc_fetch.err"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --steps 4 --warmup 1 --latency-frames 0 > /dev/null 2> "$OUT/pmc_write.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
+  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 40 --warmup 3 --latency-frames 0 \
+  > "$OUT/trace_timed_bench.json" 2> "$OUT/trace_timed.err"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $SHORT \
+  > /dev/null 2> "$OUT/pmc_fetch.err"
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 $SHORT \
+  > /dev/null 2> "$OUT/pmc_write.err"
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d "$OUT/pmc_sq_a" -o run -- python3 $SHORT \
+  > /dev/null 2> "$OUT/pmc_sq_a.err"
+timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT \
+  SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmc_sq_b" -o run \
+  -- python3 $SHORT > /dev/null 2> "$OUT/pmc_sq_b.err"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib_fetch" -o run -- \
+  $ROOT/tools/pmc_calib > "$OUT/calib_bytes.csv" 2> "$OUT/calib_fetch.err"
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o run -- \
+  $ROOT/tools/pmc_calib > /dev/null 2> "$OUT/calib_write.err"
 cd "$ROOT"
-timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-find "$OUT" -name "*.csv" | head -20
-# rocprof of the timed-region configuration only (dominant kernel timed live, no
-# serialized profile pass, no latency loop): its k_blob average is comparable
-# with bench.json's roofline.avg_launch_ms
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --steps 40 --warmup 3 --latency-frames 0 > "$OUT/trace_timed_bench.json" 2> "$OUT/trace_timed.err"
-cd "$ROOT"
+timeout -k 10 400 python3 bench.py --batch $BATCH > "$OUT/bench.json" 2> "$OUT/bench.err"
+find "$OUT" -name "*.csv" | sort
