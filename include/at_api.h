@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define AT_ABI_VERSION 2
+#define AT_ABI_VERSION 3
 
 enum {
   AT_OK = 0,
@@ -102,6 +102,13 @@ int at_detect_device(at_detector *d, const void *d_frames, size_t frame_stride, 
  * runs the host tail (reconcile + sort by id). */
 int at_enqueue_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt);
 int at_collect(at_detector *d, at_detection *out, int cap_per_frame, int *n_per_frame);
+
+/* Stream ordering without a host wait: the detector's next enqueued batch starts
+ * only after everything queued so far on `stream` (a hipStream_t of the same
+ * device, e.g. the stream a frame scatter or copy was issued on; NULL = the null
+ * stream) has completed.  Replaces a host synchronize between a producer of
+ * device-resident frames and at_enqueue_device. */
+int at_stream_wait(at_detector *d, void *stream);
 
 /* Per-frame status of the last batch: 0 or AT_E_CAPACITY (a frame whose blob
  * pair count exceeded the reference's 12-bit blob index, points.h:183-193). */

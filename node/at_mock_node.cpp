@@ -1,0 +1,142 @@
+// at_mock_node.cpp -- the node core driven from raw frame files (no ROS 2 here).
+//
+// Stands in for the subscription: every frame of --frames (back-to-back raw
+// bgr8 / yuyv / gray frames) is handed to DetectorCore::process exactly as
+// ApriltagsDetector::imageCallback hands its cv_bridge image to the detector
+// (apriltags_cuda_detector.cu:382-557).  Publishers print one JSON line per
+// frame; --proto-out / --image-out write the ApriltagListProto bytes and the
+// outlined bgr8 image of the last frame.
+//
+// usage: at_mock_node --width W --height H --format bgr8|yuyv|gray --frames F
+//        [--count N] [--calibration-dir D --camera-serial S] [--system-config C]
+//        [--measurement-csv PATH] [--proto-out P] [--image-out I] [--device K]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "at_node.h"
+
+namespace {
+struct Sink {
+  std::string robot, camera;
+};
+std::string msgs_json(const std::vector<at_node::TagDetectionMsg>& v) {
+  std::string s = "[";
+  char buf[160];
+  for (size_t i = 0; i < v.size(); ++i) {
+    std::snprintf(buf, sizeof(buf), "%s[%d,%.17g,%.17g,%.17g]", i ? "," : "", v[i].id, v[i].x, v[i].y, v[i].z);
+    s += buf;
+  }
+  return s + "]";
+}
+void on_robot(void* ctx, const std::vector<at_node::TagDetectionMsg>& v) { ((Sink*)ctx)->robot = msgs_json(v); }
+void on_camera(void* ctx, const std::vector<at_node::TagDetectionMsg>& v) { ((Sink*)ctx)->camera = msgs_json(v); }
+}  // namespace
+
+int main(int argc, char** argv) {
+  int W = 0, H = 0, count = -1, device = 0;
+  std::string fmt_s = "yuyv", frames_path, calib_dir, serial = "N/A", sys_cfg, csv, proto_out, image_out;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string k = argv[i], v = argv[i + 1];
+    if (k == "--width") W = std::atoi(v.c_str());
+    else if (k == "--height") H = std::atoi(v.c_str());
+    else if (k == "--format") fmt_s = v;
+    else if (k == "--frames") frames_path = v;
+    else if (k == "--count") count = std::atoi(v.c_str());
+    else if (k == "--calibration-dir") calib_dir = v;
+    else if (k == "--camera-serial") serial = v;
+    else if (k == "--system-config") sys_cfg = v;
+    else if (k == "--measurement-csv") csv = v;
+    else if (k == "--proto-out") proto_out = v;
+    else if (k == "--image-out") image_out = v;
+    else if (k == "--device") device = std::atoi(v.c_str());
+    else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
+  }
+  const at_pixfmt fmt = fmt_s == "bgr8" ? AT_FMT_BGR8 : (fmt_s == "gray" ? AT_FMT_GRAY8 : AT_FMT_YUYV);
+  const size_t fb = (size_t)W * H * (fmt == AT_FMT_BGR8 ? 3 : (fmt == AT_FMT_YUYV ? 2 : 1));
+  if (W <= 0 || H <= 0 || frames_path.empty()) {
+    std::fprintf(stderr, "usage: %s --width W --height H --format bgr8|yuyv|gray --frames FILE ...\n", argv[0]);
+    return 2;
+  }
+  std::ifstream in(frames_path, std::ios::binary);
+  std::vector<uint8_t> all((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  const int nframes = (int)(all.size() / fb);
+  if (count < 0 || count > nframes) count = nframes;
+
+  at_node::Params prm;
+  prm.camera_serial = serial;
+  prm.measurement_mode = !csv.empty();
+  prm.timing_csv_path = csv;
+  // the reference test camera (test/gpu_detector_test.cu:62-73) unless a calibration is given
+  at_camera cam{905.495617, 907.909470, 609.916016, 352.682645, 0.059238, -0.075154, -0.003801, 0.001113, 0.0};
+  std::string err;
+  if (!calib_dir.empty() && !at_node::load_camera_calibration(calib_dir, serial, &cam, &err)) {
+    std::fprintf(stderr, "calibration: %s\n", err.c_str());
+    return 1;
+  }
+  double R[9], t[3];
+  std::string location;
+  if (!sys_cfg.empty()) at_node::load_extrinsics(sys_cfg, serial, R, t, &location);
+  else at_node::load_extrinsics("/nonexistent", serial, R, t, &location);  // identity / zero
+  Sink sink;
+  try {
+    at_node::DetectorCore core(W, H, prm, cam, R, t, device);
+    core.publish_robot = on_robot;
+    core.publish_camera = on_camera;
+    core.ctx = &sink;
+    at_node::FrameOutputs out;
+    std::vector<uint8_t> image;
+    for (int f = 0; f < count; ++f) {
+      const double stamp = 1000.0 + 0.02 * f;
+      const int rc = core.process(all.data() + (size_t)f * fb, fmt, stamp, stamp, &out,
+                                  fmt == AT_FMT_BGR8 ? &image : nullptr);
+      if (rc != AT_OK && rc != AT_E_CAPACITY) {
+        std::fprintf(stderr, "frame %d: %s\n", f, at_strerror(rc));
+        return 1;
+      }
+      std::string dets = "[";
+      char buf[512];
+      for (size_t i = 0; i < out.detections.size(); ++i) {
+        const at_detection& d = out.detections[i];
+        std::snprintf(buf, sizeof(buf),
+                      "%s{\"id\":%d,\"hamming\":%d,\"margin\":%.9g,\"c\":[%.17g,%.17g],\"p\":[[%.17g,%.17g],[%.17g,"
+                      "%.17g],[%.17g,%.17g],[%.17g,%.17g]]}",
+                      i ? "," : "", d.id, d.hamming, d.decision_margin, d.c[0], d.c[1], d.p[0][0], d.p[0][1],
+                      d.p[1][0], d.p[1][1], d.p[2][0], d.p[2][1], d.p[3][0], d.p[3][1]);
+        dets += buf;
+      }
+      dets += "]";
+      std::string nt = "[";
+      for (size_t i = 0; i < out.networktables_pose_data.size(); ++i) {
+        std::snprintf(buf, sizeof(buf), "%s%.17g", i ? "," : "", out.networktables_pose_data[i]);
+        nt += buf;
+      }
+      nt += "]";
+      std::string hex;
+      for (unsigned char c : out.proto) {
+        std::snprintf(buf, sizeof(buf), "%02x", c);
+        hex += buf;
+      }
+      std::printf("{\"frame\":%d,\"status\":%d,\"location\":\"%s\",\"pose_topic\":\"%s\",\"camera_pose_topic\":\"%s\","
+                  "\"detections\":%s,\"robot\":%s,\"camera\":%s,\"networktables\":%s,\"proto_hex\":\"%s\"}\n",
+                  f, rc, location.c_str(), core.pose_topic().c_str(), core.camera_pose_topic().c_str(), dets.c_str(),
+                  sink.robot.c_str(), sink.camera.c_str(), nt.c_str(), hex.c_str());
+      if (f == count - 1 && !proto_out.empty()) {
+        std::ofstream po(proto_out, std::ios::binary);
+        po.write(out.proto.data(), (std::streamsize)out.proto.size());
+      }
+      if (f == count - 1 && !image_out.empty() && !image.empty()) {
+        std::ofstream io(image_out, std::ios::binary);
+        io.write((const char*)image.data(), (std::streamsize)image.size());
+      }
+    }
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -70,6 +70,7 @@ struct at_detector {
   int last_nframes;
   int pending;
   hipEvent_t ev_done;
+  hipEvent_t ev_ext;                      // at_stream_wait: recorded on the producer's stream
   int use_graphs;                         // replay the launch sequence as a hipGraph (AT_NO_GRAPH=1 disables)
   std::map<int, hipGraphExec_t> graphs;   // key: nframes * 4 + fmt
   // kernel timer under graph replay: the sequence cut around the timed kernel into
@@ -163,6 +164,7 @@ void at_destroy(at_detector* d) {
   if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
   if (d->h_dets) (void)hipHostFree(d->h_dets);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+  if (d->ev_ext) (void)hipEventDestroy(d->ev_ext);
   for (int i = 0; i <= kNumStages; i++)
     if (d->ev_stage[i]) (void)hipEventDestroy(d->ev_stage[i]);
   if (d->kt.t0) (void)hipEventDestroy(d->kt.t0);
@@ -235,6 +237,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipSetDevice(d->device) != hipSuccess) return fail(AT_E_HIP);
   if (hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
+  if (hipEventCreateWithFlags(&d->ev_ext, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   // Latency mode (max_batch < kWideBlobMaxBatch): the small-blob kernel runs on a
   // second stream beside the large-blob one.  Throughput mode: both on the one
   // stream -- concurrency comes from several detector instances (batches in
@@ -619,6 +622,14 @@ int at_enqueue_device(at_detector* d, const void* d_frames, size_t frame_stride,
   if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));  // pinned buffers are reused
   for (int f = 0; f < nframes; f++) d->h_ftab[f] = (const uint8_t*)d_frames + (size_t)f * frame_stride;
   return enqueue(d, nframes, fmt);
+}
+
+int at_stream_wait(at_detector* d, void* stream) {
+  if (!d) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipEventRecord(d->ev_ext, (hipStream_t)stream));
+  HIPCHK(hipStreamWaitEvent(d->st, d->ev_ext, 0));
+  return AT_OK;
 }
 
 int at_collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_per_frame) {

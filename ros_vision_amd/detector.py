@@ -30,7 +30,7 @@ EXPORTS = [
     "at_enqueue_device", "at_collect", "at_frame_status", "at_debug_copy", "at_destroy",
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
-    "at_set_kernel_timer", "at_kernel_time", "at_batch_stats",
+    "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -156,6 +156,7 @@ def load_library(path: str = LIB_PATH):
                                    C.c_int, C.POINTER(C.c_int)]
     L.at_enqueue_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]
     L.at_collect.argtypes = [C.c_void_p, C.POINTER(AtDetection), C.c_int, C.POINTER(C.c_int)]
+    L.at_stream_wait.argtypes = [C.c_void_p, C.c_void_p]
     L.at_frame_status.argtypes = [C.c_void_p, C.c_int]
     L.at_debug_copy.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_size_t]
     L.at_debug_copy.restype = C.c_longlong
@@ -228,7 +229,7 @@ class GpuDetector:
 
     def __init__(self, width, height, camera_matrix: CameraMatrix = TEST_CAMERA,
                  distortion_coefficients: DistCoeffs = TEST_DIST, family="tag36h11",
-                 max_batch=1, device=0, **overrides):
+                 max_batch=1, device=0, pinned_out=False, **overrides):
         L = load_library()
         self.width, self.height, self.max_batch = int(width), int(height), int(max_batch)
         cfg = AtConfig()
@@ -247,7 +248,16 @@ class GpuDetector:
         _check(L.at_create(C.byref(cfg), C.byref(cam), C.byref(h)), "at_create")
         self._h = h
         self._cap = self.MAX_DETECTIONS
-        self._out = (AtDetection * (self._cap * self.max_batch))()
+        self._out_t = None
+        if pinned_out:
+            # at_collect writes the detections straight into page-locked memory (torch owns
+            # it), so a caller can copy them to the device asynchronously without staging
+            import torch
+            nb = C.sizeof(AtDetection) * self._cap * self.max_batch
+            self._out_t = torch.empty(nb, dtype=torch.uint8).pin_memory()
+            self._out = (AtDetection * (self._cap * self.max_batch)).from_address(self._out_t.data_ptr())
+        else:
+            self._out = (AtDetection * (self._cap * self.max_batch))()
         self._n = (C.c_int * self.max_batch)()
         self._last = [[] for _ in range(self.max_batch)]
         self._last_status = 0
@@ -316,6 +326,11 @@ class GpuDetector:
         _check(load_library().at_enqueue_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt),
                "at_enqueue_device")
         self._pending = nframes
+
+    def wait_stream(self, stream_handle: int):
+        """at_stream_wait: the next enqueued batch waits (on the GPU) for the work queued
+        so far on a HIP stream, e.g. torch.cuda.current_stream().cuda_stream."""
+        _check(load_library().at_stream_wait(self._h, C.c_void_p(stream_handle)), "at_stream_wait")
 
     def poses(self, frame=0):
         """Pose of each detection of `frame` of the last batch (same order as its
@@ -431,7 +446,7 @@ class GpuDetector:
         return self._copy(AT_STAGE_BLOB_POINTS, frame, need, np.uint64)
 
     def copy_quads(self, frame=0):
-        recs = (AtQuadRecord * 2048)()
+        recs = (AtQuadRecord * 4096)()
         n = load_library().at_debug_copy(self._h, AT_STAGE_QUADS, frame, C.cast(recs, C.c_void_p), C.sizeof(recs))
         _check(int(n), "at_debug_copy")
         out = []

@@ -105,12 +105,19 @@ class ScatterIngest:
         i = step % 2
         self.work[i] = self.dist.scatter(self.buf[i], scatter_list=self._chunks(step), src=0, async_op=True)
 
-    def ready(self, step):
+    def ready(self, step, detector=None):
+        """Buffer of step `step`.  On the GPU the collective's completion is handed to
+        `detector`'s stream as a stream dependency (at_stream_wait), not a host wait;
+        without a detector the host synchronizes torch's stream."""
         import torch
         i = step % 2
-        self.work[i].wait()
+        self.work[i].wait()  # torch's current stream now waits for the collective
         if self.buf[i].is_cuda:
-            torch.cuda.current_stream(self.buf[i].device).synchronize()  # detector streams are not torch's
+            stream = torch.cuda.current_stream(self.buf[i].device)
+            if detector is not None:
+                detector.wait_stream(stream.cuda_stream)
+            else:
+                stream.synchronize()
         return self.buf[i]
 
 

@@ -1,0 +1,199 @@
+"""The compiled side of the boundary and the C++ node adapter.
+
+CPU: node/abi_check (plain C11 consumer of include/at_api.h, struct layouts pinned by
+_Static_assert) against the ctypes mirror; the ApriltagListProto bytes of the C++ core
+parsed by google.protobuf against the reference schema (proto/apriltag.proto:6-17);
+calibration / extrinsics loaders against the Python node; the outline drawing.
+GPU: abi_check and at_mock_node detect through the C ABI and agree with the Python
+binding, the Python node and the oracle.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NODE = os.path.join(ROOT, "node")
+
+
+@pytest.fixture(scope="module")
+def built():
+    subprocess.run(["make", "-C", NODE, "-s"], check=True)
+    return NODE
+
+
+@pytest.fixture(scope="module")
+def nodelib(built):
+    from ros_vision_amd import detector
+    detector.load_library()  # libat_hip first (torch owns the HIP runtime when present)
+    L = C.CDLL(os.path.join(built, "libat_node.so"))
+    L.at_node_encode_apriltag_list.restype = C.c_longlong
+    L.at_node_encode_apriltag_list.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_size_t]
+    L.at_node_load_camera_calibration.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(detector.AtCamera)]
+    L.at_node_load_extrinsics.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                          C.c_char_p, C.c_size_t]
+    L.at_node_draw_detection_outlines.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    return L
+
+
+def proto_classes():
+    """ApriltagProto / ApriltagListProto built from the reference schema (proto2)."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+    F = descriptor_pb2.FieldDescriptorProto
+    fdp = descriptor_pb2.FileDescriptorProto(name="apriltag.proto", package="com.team766.vision", syntax="proto2")
+    m = fdp.message_type.add(name="ApriltagProto")
+    for name, num, typ in [("collect_time", 1, F.TYPE_DOUBLE), ("tag_id", 2, F.TYPE_INT32), ("x", 3, F.TYPE_DOUBLE),
+                           ("y", 4, F.TYPE_DOUBLE), ("z", 5, F.TYPE_DOUBLE)]:
+        m.field.add(name=name, number=num, type=typ, label=F.LABEL_REQUIRED)
+    ml = fdp.message_type.add(name="ApriltagListProto")
+    ml.field.add(name="tags", number=1, type=F.TYPE_MESSAGE, label=F.LABEL_REPEATED,
+                 type_name=".com.team766.vision.ApriltagProto")
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    get = getattr(message_factory, "GetMessageClass", None)
+    if get is None:
+        get = message_factory.MessageFactory(pool).GetPrototype
+    return get(pool.FindMessageTypeByName("com.team766.vision.ApriltagListProto"))
+
+
+def test_abi_layout_matches_ctypes_mirror(built):
+    from ros_vision_amd import detector as D
+    lay = json.loads(subprocess.run([os.path.join(built, "abi_check"), "layout"], check=True, capture_output=True,
+                                    text=True).stdout)
+    assert lay["abi_version"] == lay["library_abi_version"] == D.load_library().at_abi_version()
+    for cname, ct in [("at_config", D.AtConfig), ("at_camera", D.AtCamera), ("at_detection", D.AtDetection),
+                      ("at_pose", D.AtPose), ("at_tag_detection", D.AtTagDetection),
+                      ("at_quad_record", D.AtQuadRecord)]:
+        assert lay["sizeof." + cname] == C.sizeof(ct), cname
+        for fname, _ in ct._fields_:
+            assert lay["%s.%s" % (cname, fname)] == getattr(ct, fname).offset, (cname, fname)
+
+
+def test_apriltag_list_proto_bytes(nodelib):
+    from ros_vision_amd import detector as D
+    tags = (D.AtTagDetection * 3)()
+    vals = [(7, (0.5, -1.25, 3.0)), (586, (1e-9, 2.5, -0.0)), (-3, (12.0, 0.1, 1.0))]
+    for i, (tid, r) in enumerate(vals):
+        tags[i].id = tid
+        tags[i].robot[:] = list(r)
+    buf = (C.c_uint8 * 1024)()
+    n = nodelib.at_node_encode_apriltag_list(tags, 3, 1234.5678, buf, 1024)
+    raw = bytes(buf[:n])
+    Msg = proto_classes()
+    msg = Msg()
+    msg.ParseFromString(raw)
+    assert [t.tag_id for t in msg.tags] == [7, 586, -3]
+    for t, (tid, r) in zip(msg.tags, vals):
+        assert t.collect_time == 1234.5678 and (t.x, t.y, t.z) == r
+    assert msg.SerializeToString() == raw  # same bytes as the protobuf runtime writes
+    assert nodelib.at_node_encode_apriltag_list(tags, 0, 0.0, buf, 1024) == 0  # no tags: empty message
+
+
+def test_calibration_and_extrinsics_match_python_node(nodelib, tmp_path):
+    from ros_vision_amd import detector as D
+    from ros_vision_amd import node as N
+    (tmp_path / "calibrationmatrix_CAM1.json").write_text(json.dumps(
+        {"matrix": [[905.5, 0, 609.9], [0, 907.9, 352.7], [0, 0, 1]], "disto": [[0.05, -0.07, -0.003, 0.001, 0.02]]}))
+    cam = D.AtCamera()
+    assert nodelib.at_node_load_camera_calibration(str(tmp_path).encode(), b"CAM1", C.byref(cam)) == 0
+    pc, pd = N.load_camera_calibration(str(tmp_path), "CAM1")
+    assert (cam.fx, cam.fy, cam.cx, cam.cy) == (pc.fx, pc.fy, pc.cx, pc.cy)
+    assert (cam.k1, cam.k2, cam.p1, cam.p2, cam.k3) == (pd.k1, pd.k2, pd.p1, pd.p2, pd.k3)
+    assert nodelib.at_node_load_camera_calibration(str(tmp_path).encode(), b"NOPE", C.byref(cam)) != 0
+    rot = [[0, -1, 0], [1, 0, 0], [0, 0, 1]]
+    cfg = {"camera_mounted_positions": {"CAM1": "front", "CAM2": {"location": "back"}, "CAM3": "side"},
+           "extrinsics": {"front": {"rotation": rot, "offset": [0.1, 0.2, 0.3]},
+                          "back": {"rotation": sum(rot, []), "offset": [-1, 0, 2]}}}
+    path = tmp_path / "system_config.json"
+    path.write_text(json.dumps(cfg))
+    for serial, ok in [("CAM1", 0), ("CAM2", 0), ("CAM3", -1), ("CAM9", -1)]:
+        R, t = (C.c_double * 9)(), (C.c_double * 3)()
+        loc = C.create_string_buffer(64)
+        assert nodelib.at_node_load_extrinsics(str(path).encode(), serial.encode(), R, t, loc, 64) == ok
+        pR, pt, ploc = N.load_extrinsics(str(path), serial)
+        assert np.array_equal(np.array(list(R)).reshape(3, 3), pR) and np.array_equal(np.array(list(t)), pt)
+        assert (loc.value.decode() or None) == ploc
+
+
+def test_outlines_and_id_text(nodelib):
+    from ros_vision_amd import detector as D
+    W, H = 320, 240
+    img = np.zeros((H, W, 3), np.uint8)
+    det = (D.AtDetection * 1)()
+    det[0].id = 42
+    pts = [(100.7, 60.2), (220.3, 60.9), (220.9, 180.4), (100.1, 180.8)]
+    for k, (x, y) in enumerate(pts):
+        det[0].p[k][0], det[0].p[k][1] = x, y
+    det[0].c[0], det[0].c[1] = 160.0, 120.0
+    nodelib.at_node_draw_detection_outlines(img.ctypes.data, W, H, det, 1)
+    assert tuple(img[60, 160]) == (0, 255, 0)      # p0-p1 green (BGR)
+    assert tuple(img[120, 100]) == (0, 0, 255)     # p0-p3 red
+    assert tuple(img[120, 220]) == (255, 0, 0)     # p1-p2 blue
+    assert tuple(img[180, 160]) == (255, 0, 0)     # p2-p3 blue
+    text = np.all(img[100:140, 130:190] == (255, 153, 0), axis=-1)
+    assert text.sum() > 40                         # the id, centred on c
+
+
+# ---- GPU: the compiled consumers detect through the C ABI --------------------
+
+@pytest.mark.gpu
+def test_abi_check_detects_reference_fixture(built, golden_dir, tmp_path):
+    from PIL import Image
+    y = np.asarray(Image.open(os.path.join(golden_dir, "colorimage_y.png")))
+    f = tmp_path / "frame.raw"
+    y.tofile(f)
+    out = subprocess.run([os.path.join(built, "abi_check"), "detect", str(y.shape[1]), str(y.shape[0]), "2", str(f)],
+                         check=True, capture_output=True, text=True, timeout=120).stdout
+    dets = json.loads(out)
+    assert [d["id"] for d in dets] == [554]
+
+
+@pytest.mark.gpu
+def test_mock_node_matches_python_node_and_oracle(built, oracle_mod, tmp_path):
+    import ros_vision_amd as rva
+    from ros_vision_amd import node as N
+    from ros_vision_amd import synth
+    W, H = 1280, 720
+    frames = [synth.stream_frame(W, H, f)[1] for f in (3, 33)]
+    bgr = np.stack([np.repeat(g[:, :, None], 3, axis=2) for g in frames])  # gray scene as bgr8
+    path = tmp_path / "frames.raw"
+    bgr.tofile(path)
+    rot = [[0, 0, 1], [-1, 0, 0], [0, -1, 0]]
+    cfg = tmp_path / "system_config.json"
+    cfg.write_text(json.dumps({"camera_mounted_positions": {"S1": "front"},
+                               "extrinsics": {"front": {"rotation": rot, "offset": [0.2, 0.0, 0.5]}}}))
+    csv = tmp_path / "timing.csv"
+    proto = tmp_path / "last.pb"
+    out = subprocess.run([os.path.join(built, "at_mock_node"), "--width", str(W), "--height", str(H), "--format",
+                          "bgr8", "--frames", str(path), "--camera-serial", "S1", "--system-config", str(cfg),
+                          "--measurement-csv", str(csv), "--proto-out", str(proto)],
+                         check=True, capture_output=True, text=True, timeout=180).stdout
+    lines = [json.loads(l) for l in out.splitlines()]
+    assert len(lines) == 2
+    node = N.ApriltagsDetectorNode(W, H, parameters={"camera_serial": "S1"}, system_config_path=str(cfg))
+    Msg = proto_classes()
+    for i, rec in enumerate(lines):
+        assert rec["status"] == 0 and rec["location"] == "front" and rec["camera_pose_topic"] == "camera/pose_camera"
+        orc = oracle_mod.Oracle(W, H)
+        orc.detect(bgr[i], rva.AT_FMT_BGR8)
+        want = orc.detections()
+        assert [d["id"] for d in rec["detections"]] == [d["id"] for d in want] and len(want) == 15
+        for a, b in zip(rec["detections"], want):
+            assert np.allclose(a["p"], b["p"], atol=1e-4)
+        res = node.image_callback(bgr[i], 1000.0 + 0.02 * i)
+        assert [r[0] for r in rec["robot"]] == [r[0] for r in res.tag_detection_array]
+        assert np.allclose(np.array(rec["robot"]), np.array(res.tag_detection_array), atol=1e-12)
+        assert np.allclose(np.array(rec["camera"]), np.array(res.tag_detection_camera_array), atol=1e-12)
+        assert np.allclose(rec["networktables"], res.networktables_pose_data, atol=1e-12)
+        msg = Msg()
+        msg.ParseFromString(bytes.fromhex(rec["proto_hex"]))
+        assert [t.tag_id for t in msg.tags] == [r[0] for r in rec["robot"]]
+        assert all(t.collect_time == 1000.0 + 0.02 * i for t in msg.tags)
+    node.close()
+    assert proto.read_bytes() == bytes.fromhex(lines[-1]["proto_hex"])
+    rows = csv.read_text().splitlines()
+    assert rows[0].startswith("latency_us,det_time_us") and len(rows) == 3
