@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=128, help="frames per step per GPU")
     ap.add_argument("--pool", type=int, default=64, help="distinct synthetic frames per GPU")
     ap.add_argument("--hbm-copies", type=int, default=4,
                     help="copies of the frame pool in HBM (4 x 64 frames = 0.47 GB at 720p, more than the "
@@ -50,9 +50,9 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--tags", type=int, default=15)
     ap.add_argument("--latency-frames", type=int, default=1000)
-    ap.add_argument("--instances", type=int, default=8,
+    ap.add_argument("--instances", type=int, default=4,
                     help="detector instances (one HIP stream each) used round-robin, i.e. batches in flight")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
                          "detector stream so the batches in flight run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")

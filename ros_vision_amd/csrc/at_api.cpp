@@ -21,6 +21,9 @@
 
 namespace at {
 hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
+hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint32_t* size, uint32_t* out, int Wd,
+                            int Hd, hipStream_t st);
+hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd, hipStream_t st);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt);
@@ -198,8 +201,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.W = W; g.H = H; g.Wd = W / 2; g.Hd = H / 2;
   g.TW = g.Wd / 4; g.TH = g.Hd / 4;
   g.BW = g.Wd / 2; g.BH = g.Hd / 2;
-  g.CTX = (g.Wd + kCclTile - 1) / kCclTile;
-  g.CTY = (g.Hd + kCclTile - 1) / kCclTile;
+  g.CTX = (g.Wd + kCclTileW - 1) / kCclTileW;
+  g.CTY = (g.Hd + kCclTileH - 1) / kCclTileH;
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
   g.BTX = (g.Wd - 2 + 63) / 64;
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
@@ -757,34 +760,29 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
     case AT_STAGE_DECIMATED: src = d->d.dec + frame * nd; n = nd; break;
     case AT_STAGE_THRESHOLD: src = d->d.thr + frame * nd; n = nd; break;
     case AT_STAGE_LABELS: {
-      // LabelImage's output (labeling_allegretti_2019_BKE.cu:340-462) resolved
-      // from the union-find forest: label = par[par[node]] (node -> local root ->
-      // component root); 127 -> 0; a block of four 127 pixels -> the pixel index
+      // LabelImage's output (labeling_allegretti_2019_BKE.cu:340-462), resolved from
+      // the union-find forest on the device (k_tap_labels)
       if (bytes < nd * 4) return AT_E_INVALID;
-      std::vector<uint8_t> t(nd);
-      std::vector<uint32_t> par(nd);
-      if (hipMemcpy(t.data(), d->d.thr + frame * nd, nd, hipMemcpyDeviceToHost) != hipSuccess ||
-          hipMemcpy(par.data(), d->d.par + frame * nd, nd * 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return AT_E_HIP;
-      uint32_t* lab = (uint32_t*)dst;
-      const int Wd = g.Wd;
-      for (int y = 0; y < g.Hd; y++)
-        for (int x = 0; x < Wd; x++) {
-          const size_t i = (size_t)y * Wd + x;
-          const size_t F = (size_t)(y & ~1) * Wd + (x & ~1);
-          const bool all127 = t[F] == 127 && t[F + 1] == 127 && t[F + Wd] == 127 && t[F + Wd + 1] == 127;
-          if (all127) {
-            lab[i] = (uint32_t)i;
-          } else if (t[i] == 127) {
-            lab[i] = 0;
-          } else {
-            const size_t node = t[i] == 255 ? F : F + Wd + (x & 1);
-            lab[i] = par[par[node]];
-          }
-        }
-      return (long long)(nd * 4);
+      uint32_t* tmp_d = nullptr;
+      if (hipMalloc(&tmp_d, nd * 4) != hipSuccess) return AT_E_NOMEM;
+      hipError_t e = launch_tap_labels(d->d.thr + frame * nd, d->d.par + frame * nd, tmp_d, g.Wd, g.Hd, d->st);
+      if (e == hipSuccess) e = hipStreamSynchronize(d->st);
+      if (e == hipSuccess) e = hipMemcpy(dst, tmp_d, nd * 4, hipMemcpyDeviceToHost);
+      (void)hipFree(tmp_d);
+      return e == hipSuccess ? (long long)(nd * 4) : AT_E_HIP;
     }
-    case AT_STAGE_SIZES: src = d->d.size + frame * nd; n = nd * 4; break;
+    case AT_STAGE_SIZES: {
+      // the dense plane of the reference, masked from the forest on the device
+      if (bytes < nd * 4) return AT_E_INVALID;
+      uint32_t* tmp_d = nullptr;
+      if (hipMalloc(&tmp_d, nd * 4) != hipSuccess) return AT_E_NOMEM;
+      hipError_t e = launch_tap_sizes(d->d.thr + frame * nd, d->d.par + frame * nd, d->d.size + frame * nd, tmp_d,
+                                      g.Wd, g.Hd, d->st);
+      if (e == hipSuccess) e = hipStreamSynchronize(d->st);
+      if (e == hipSuccess) e = hipMemcpy(dst, tmp_d, nd * 4, hipMemcpyDeviceToHost);
+      (void)hipFree(tmp_d);
+      return e == hipSuccess ? (long long)(nd * 4) : AT_E_HIP;
+    }
     case AT_STAGE_NUM_POINTS:
       if (bytes < 4) return AT_E_INVALID;
       memcpy(dst, &d->h_ctrl[kCtlNpts * B + frame], 4);

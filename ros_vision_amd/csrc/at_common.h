@@ -9,10 +9,19 @@
 namespace at {
 
 // ---- capacities -----------------------------------------------------------
-constexpr int kCclTile = 32;           // CCL tile edge in decimated pixels (16x16 2x2-blocks)
-constexpr int kCclTileNodes = 768;     // union-find nodes of one CCL tile (3 per 2x2 block)
-constexpr int kHashSlots = 8192;       // per-frame open-addressing table of blob pairs (<= 50% full)
-constexpr int kHashBits = 13;
+// CCL tile: 64 x 32 decimated pixels = 32 x 16 2x2-blocks per 512-thread workgroup
+// (one thread per block): twice the pixels per workgroup of a 32 x 32 tile for the
+// same dependent round trips, and a third fewer tile-border unions per pixel
+constexpr int kCclTileW = 64;
+constexpr int kCclTileH = 32;
+constexpr int kCclBW = kCclTileW / 2, kCclBH = kCclTileH / 2;  // blocks per tile row / column
+constexpr int kCclThreads = kCclBW * kCclBH;                  // 512
+constexpr int kCclTileNodes = 3 * kCclThreads;                 // union-find nodes of one CCL tile
+// per-frame open-addressing table of blob pairs: 4096 slots hold every frame the
+// 12-bit blob index admits (<= kMaxPairs keys; typical frames fill ~10 %), and keep
+// k_pairs' LDS copy at 84 KB so it co-resides with other kernels' workgroups
+constexpr int kHashSlots = 4096;
+constexpr int kHashBits = 12;
 constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count) entries (tiles with > kLdsPairSlots pairs)
 // k_boundary tiles: 64 x (4 * kBndRows) interior pixels per 256-thread workgroup;
 // each tile owns a fixed region of kBndPts points and kLdsPairSlots pair entries
@@ -111,7 +120,9 @@ struct DevDetection {
   double pose_err[2];  // errors of the first / second minimum (HUGE_VAL: none)
 };
 
-// Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode.
+// Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode;
+// every kept blob reserves a slot, frame == kQuadInvalid marks a rejected quad.
+constexpr uint32_t kQuadInvalid = 0xffffffffu;
 struct QuadCand {
   uint32_t frame, rank;
   float p[4][2];

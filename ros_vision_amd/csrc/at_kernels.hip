@@ -231,9 +231,9 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
 
 // ---------------------------------------------------------------------------
 // K3: threshold + tile-local union-find.
-// One 256-thread workgroup per 32x32 decimated tile; thread (ty,tx) owns
+// One 512-thread workgroup per 64x32 decimated tile; thread (ty,tx) owns
 // 2x2 block (ty,tx).  Node slots in LDS are ordered like the global node ids
-// (per block row: 16 foreground nodes, then 32 background L/R nodes), so
+// (per block row: 32 foreground nodes, then 64 background L/R nodes), so
 // "link to the smaller slot" == "link to the smaller id" and every local root
 // is the minimum node id of its local component.
 // ---------------------------------------------------------------------------
@@ -268,40 +268,44 @@ __device__ __forceinline__ void lds_union(uint32_t* par, uint32_t a, uint32_t b)
   }
 }
 
+constexpr int kCclRowNodes = 3 * kCclBW;  // node slots per block row
 __device__ __forceinline__ uint32_t slot_of(int ty, int tx, int type) {
-  return (uint32_t)(ty * 48 + (type == 0 ? tx : 16 + 2 * tx + (type - 1)));
+  return (uint32_t)(ty * kCclRowNodes + (type == 0 ? tx : kCclBW + 2 * tx + (type - 1)));
 }
 
-__global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
+__global__ __launch_bounds__(kCclThreads) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
+  constexpr int NT = kCclThreads;
+  constexpr int kTW = kCclTileW / 4, kTH = kCclTileH / 4;  // 4x4 threshold tiles per CCL tile
+  constexpr int kHR = kCclTileH + 1, kHC = kCclTileW + 2;  // threshold halo: rows y0-1.., cols x0-1..x0+W
   const int f = blockIdx.z;
   const int tid = threadIdx.x;
-  const int y0 = blockIdx.y * kCclTile, x0 = blockIdx.x * kCclTile;
+  const int y0 = blockIdx.y * kCclTileH, x0 = blockIdx.x * kCclTileW;
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
   const uint8_t* mm = b.mm + (size_t)f * g.TW * g.TH * 2;
   uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
 
-  __shared__ uint8_t s_umn[11][12], s_umx[11][12];
-  __shared__ uint8_t s_fmn[9][10], s_fmx[9][10];
-  __shared__ uint8_t s_t[33][36];  // thr of rows y0-1..y0+31, cols x0-1..x0+32 (+pad)
-  __shared__ uint32_t s_par[768];
-  __shared__ uint32_t s_cnt[768];
+  __shared__ uint8_t s_umn[kTH + 3][kTW + 4], s_umx[kTH + 3][kTW + 4];
+  __shared__ uint8_t s_fmn[kTH + 1][kTW + 2], s_fmx[kTH + 1][kTW + 2];
+  __shared__ uint8_t s_t[kHR][kHC + 2];  // thr of rows y0-1..y0+H-1, cols x0-1..x0+W (+pad)
+  __shared__ uint32_t s_par[kCclTileNodes];
+  __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
   if (tid == 0) s_nlr = 0;
 
-  // unfiltered tile min/max for tile rows ty0-2..ty0+8, cols tx0-2..tx0+9
+  // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   // the tile's decimated pixels (+1 halo) are loaded together with the tile
   // min/max: one global round trip instead of two
-  constexpr int kDecPer = (33 * 34 + 255) / 256;
+  constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
   uint8_t dv[kDecPer];
 #pragma unroll
   for (int k = 0; k < kDecPer; k++) {
-    const int i = tid + 256 * k;
-    const int y = y0 - 1 + i / 34, x = x0 - 1 + i % 34;
-    dv[k] = (i < 33 * 34 && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? dec[(size_t)y * g.Wd + x] : 0;
+    const int i = tid + NT * k;
+    const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
+    dv[k] = (i < kHR * kHC && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? dec[(size_t)y * g.Wd + x] : 0;
   }
-  for (int i = tid; i < 11 * 12; i += 256) {
-    const int r = i / 12, c = i % 12;
+  for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
+    const int r = i / (kTW + 4), c = i % (kTW + 4);
     const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
     uint8_t mn = 255, mx = 0;  // out of range: neutral for min/max
     if (tr >= 0 && tr < g.TH && tc >= 0 && tc < g.TW) {
@@ -313,9 +317,9 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     s_umx[r][c] = mx;
   }
   __syncthreads();
-  // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+7
-  for (int i = tid; i < 9 * 10; i += 256) {
-    const int r = i / 10, c = i % 10;
+  // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+kTH-1
+  for (int i = tid; i < (kTH + 1) * (kTW + 2); i += NT) {
+    const int r = i / (kTW + 2), c = i % (kTW + 2);
     uint8_t mn = 255, mx = 0;
 #pragma unroll
     for (int dr = 0; dr < 3; dr++)
@@ -328,12 +332,12 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     s_fmx[r][c] = mx;
   }
   __syncthreads();
-  // InternalThreshold for the 33x34 halo region; outside the image -> 127
+  // InternalThreshold for the halo region; outside the image -> 127
 #pragma unroll
   for (int k = 0; k < kDecPer; k++) {
-    const int i = tid + 256 * k;
-    if (i < 33 * 34) {
-      const int r = i / 34, c = i % 34;
+    const int i = tid + NT * k;
+    if (i < kHR * kHC) {
+      const int r = i / kHC, c = i % kHC;
       const int y = y0 - 1 + r, x = x0 - 1 + c;
       uint8_t res = 127;
       if (y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) {
@@ -349,14 +353,14 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
       s_t[r][c] = res;
     }
   }
-  for (int i = tid; i < 768; i += 256) {
+  for (int i = tid; i < kCclTileNodes; i += NT) {
     s_par[i] = i;
     s_cnt[i] = 0;
   }
   __syncthreads();
   // write this tile's threshold plane (4 bytes per thread)
   {
-    const int r = tid >> 3, c4 = (tid & 7) * 4;
+    const int r = tid / (kCclTileW / 4), c4 = (tid % (kCclTileW / 4)) * 4;
     const int y = y0 + r, x = x0 + c4;
     if (y < g.Hd && x < g.Wd) {
       const uint32_t w = s_t[r + 1][c4 + 1] | (s_t[r + 1][c4 + 2] << 8) | (s_t[r + 1][c4 + 3] << 16) |
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     }
   }
   // local unions over intra-tile edges (InitLabeling P/Q/R/S + Merge)
-  const int bty = tid >> 4, btx = tid & 15;
+  const int bty = tid / kCclBW, btx = tid % kCclBW;
 #define T(rr, cc) s_t[(rr) + 1][(cc) + 1]
   const int pr = 2 * bty, pc = 2 * btx;
   const uint8_t a = T(pr, pc), bb = T(pr, pc + 1), c = T(pr + 1, pc), d = T(pr + 1, pc + 1);
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     if (btx > 0 && a == 255 && T(pr - 1, pc - 1) == 255) lds_union(s_par, F, slot_of(bty - 1, btx - 1, 0));
     if ((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255))
       lds_union(s_par, F, slot_of(bty - 1, btx, 0));
-    if (btx < 15 && bb == 255 && T(pr - 1, pc + 2) == 255) lds_union(s_par, F, slot_of(bty - 1, btx + 1, 0));
+    if (btx < kCclBW - 1 && bb == 255 && T(pr - 1, pc + 2) == 255) lds_union(s_par, F, slot_of(bty - 1, btx + 1, 0));
     if (a == 0 && T(pr - 1, pc) == 0) lds_union(s_par, L, slot_of(bty - 1, btx, 1));
     if (bb == 0 && T(pr - 1, pc + 1) == 0) lds_union(s_par, R, slot_of(bty - 1, btx, 2));
   }
@@ -402,10 +406,10 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
   if (BY < g.BH && BX < g.BW) {
     auto gid = [&](uint32_t s) -> uint32_t {
-      const int sty = s / 48, r = s % 48;
+      const int sty = s / kCclRowNodes, r = s % kCclRowNodes;
       const int gy = y0 / 2 + sty;
-      if (r < 16) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
-      const int k = r - 16;
+      if (r < kCclBW) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
+      const int k = r - kCclBW;
       return (uint32_t)((2 * gy + 1) * g.Wd + 2 * (x0 / 2 + (k >> 1)) + (k & 1));
     };
     uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -414,14 +418,22 @@ __global__ __launch_bounds__(256) void k_thr_ccl(DevBufs b, Geom g, Params prm) 
     const uint32_t idL = idF + g.Wd;
     *reinterpret_cast<uint2*>(par + idF) = make_uint2(gid(rF), idF + 1);
     *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL), gid(rR));
-    *reinterpret_cast<uint2*>(size + idF) = make_uint2(rF == F ? s_cnt[F] : 0u, 0u);
-    *reinterpret_cast<uint2*>(size + idL) = make_uint2(rL == L ? s_cnt[L] : 0u, rR == R ? s_cnt[R] : 0u);
+    // sizes only at local roots with pixels: every other entry is never read
+    // (k_boundary reads component roots, k_ccl_roots the listed local roots; the
+    // AT_STAGE_SIZES tap masks the plane with the forest, k_tap_sizes)
+    const uint32_t cF = rF == F ? s_cnt[F] : 0u, cL = rL == L ? s_cnt[L] : 0u, cR = rR == R ? s_cnt[R] : 0u;
+    if (cF) size[idF] = cF;
+    if (cL | cR) {
+      if (cL && cR) *reinterpret_cast<uint2*>(size + idL) = make_uint2(cL, cR);
+      else if (cL) size[idL] = cL;
+      else size[idL + 1] = cR;
+    }
     // the tile's local roots (components with pixels), for k_ccl_roots
     const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
     uint32_t* lr = b.lroot + tl * kCclTileNodes;
-    if (rF == F && s_cnt[F]) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
-    if (rL == L && s_cnt[L]) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
-    if (rR == R && s_cnt[R]) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
+    if (cF) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
+    if (cL) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
+    if (cR) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
   if (tid == 0) b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
@@ -487,20 +499,22 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
 }
 
 // One candidate union per thread (the reference's Merge, labeling_allegretti_2019_BKE.cu:302-338,
-// over the tile's border blocks): threads 0-79 the top block row (16 blocks x
-// P, Q, R and the two background links), 80-127 the left block column (16 x P,
-// S, background S), 128-142 the right column (15 x R).  Every union is one
-// short chain of global round trips instead of up to five in a row per lane.
-constexpr int kBorderThreads = 192;
+// over the tile's border blocks): threads 0..5*BW-1 the top block row (BW blocks x
+// P, Q, R and the two background links), then the left block column (BH x P, S,
+// background S), then the right column (BH-1 x R).  Every union is one short
+// chain of global round trips instead of up to five in a row per lane.
+constexpr int kBorderTop = 5 * kCclBW, kBorderLeft = 3 * kCclBH, kBorderRight = kCclBH - 1;
+constexpr int kBorderThreads = (kBorderTop + kBorderLeft + kBorderRight + 63) / 64 * 64;
 __global__ __launch_bounds__(kBorderThreads) void k_ccl_border(DevBufs b, Geom g) {
   const int f = blockIdx.z;
   const int t = threadIdx.x;
   int bty, btx, role, kind;
-  if (t < 80) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
-  else if (t < 128) { role = 1; bty = (t - 80) / 3; btx = 0; kind = (t - 80) % 3; }
-  else if (t < 143) { role = 2; bty = t - 127; btx = 15; kind = 0; }
-  else return;
-  const int BY = blockIdx.y * 16 + bty, BX = blockIdx.x * 16 + btx;
+  if (t < kBorderTop) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
+  else if (t < kBorderTop + kBorderLeft) { role = 1; bty = (t - kBorderTop) / 3; btx = 0; kind = (t - kBorderTop) % 3; }
+  else if (t < kBorderTop + kBorderLeft + kBorderRight) {
+    role = 2; bty = t - (kBorderTop + kBorderLeft) + 1; btx = kCclBW - 1; kind = 0;
+  } else return;
+  const int BY = blockIdx.y * kCclBH + bty, BX = blockIdx.x * kCclBW + btx;
   if (BY >= g.BH || BX >= g.BW) return;
   const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -561,8 +575,7 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
     if (r != l) {
       par[l] = r;  // unions are over: a concurrent find sees the old parent or r, both lead to r
       const uint32_t cnt = size[l];
-      atomicAdd(size + r, cnt);  // result unused: no round trip
-      size[l] = 0;
+      atomicAdd(size + r, cnt);  // result unused: no round trip (size[l] is dead from here on)
     }
   }
 }
@@ -832,7 +845,6 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __shared__ uint64_t t_key[kHashSlots];
   __shared__ uint32_t t_cnt[kHashSlots];
   __shared__ uint64_t s_list[kMaxPairs];
-  __shared__ uint32_t s_cnt[kMaxPairs];
   __shared__ uint32_t s_n, s_full, s_np;
   __shared__ uint32_t s_wsum[16];
   for (int i = tid; i < kHashSlots; i += 1024) {
@@ -939,12 +951,11 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     block_bitonic_sort<uint64_t, 1024>(s_list, np2);
   }
   stamp(3);
-  // counts in rank order, exclusive scan -> offsets
-  for (int i = tid; i < kMaxPairs; i += 1024) s_cnt[i] = i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u;
-  __syncthreads();
+  // counts in rank order (straight from the hash slots), exclusive scan -> offsets;
   // each thread owns 4 consecutive ranks
   const int i0 = tid * 4;
-  const uint32_t c0 = s_cnt[i0], c1 = s_cnt[i0 + 1], c2 = s_cnt[i0 + 2], c3 = s_cnt[i0 + 3];
+  auto cnt_at = [&](int i) -> uint32_t { return i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u; };
+  const uint32_t c0 = cnt_at(i0), c1 = cnt_at(i0 + 1), c2 = cnt_at(i0 + 2), c3 = cnt_at(i0 + 3);
   const uint32_t tsum = c0 + c1 + c2 + c3;
   const uint32_t incl = wave_incl_scan(tsum, AddOp(), 0u);
   const uint32_t lane = lane_id();
@@ -1880,9 +1891,20 @@ __device__ __forceinline__ Mom6 prefix_at(const BlobShared<NT, CAP>& S, const ui
 // Processes one work item (frame, pair rank) with a team of NT threads.
 // gpk: this team's global overflow area for peak keys beyond kPeakCap (large
 // blobs only; nullptr when the LDS area always suffices).
+// A work item's pair-table entries (count, segment offset, SelectBlobs flag),
+// loaded one item ahead by the persistent loops so their round trip overlaps
+// the previous blob's work.
+struct PairInfo {
+  uint32_t n, off, sel;
+};
+__device__ __forceinline__ PairInfo load_pair_info(const DevBufs& b, uint32_t w) {
+  const size_t i = (size_t)(w >> 16) * kMaxPairs + (w & 0xffff);
+  return PairInfo{b.pair_cnt[i], b.pair_off[i], b.pair_sel[i]};
+}
+
 template <int NT, int CAP>
 __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S, uint64_t* gpk,
-                          const uint32_t* combo, uint32_t w, uint32_t* pacc) {
+                          const uint32_t* combo, uint32_t w, PairInfo pi_, uint32_t* pacc) {
   constexpr int kC = (CAP + NT - 1) / NT;  // max points per thread chunk
   constexpr int kPk = kPeakCap<CAP>;
   constexpr bool kGlobPk = kPk < CAP / 2;  // peaks (<= n/2) may overflow the LDS area
@@ -1909,16 +1931,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   };
   const int f = (int)(w >> 16);
   const uint32_t rank = w & 0xffff;
-  const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
+  const uint32_t n = pi_.n;
   big = n > 2048;
-  const uint32_t off = b.pair_off[(size_t)f * kMaxPairs + rank];
-  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + off;
-  const uint32_t sel = b.pair_sel[(size_t)f * kMaxPairs + rank];
-  // the three loads in one round trip: n and off are needed before the branch
-  asm volatile("" ::"v"(n), "v"(off));
+  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + pi_.off;
 
   // extents, SelectBlobs and the theta keys come from k_extents
-  if (sel == 0) return;  // uniform across the team
+  if (pi_.sel == 0) return;  // uniform across the team
+
   if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
   const uint32_t bi = rank & 0xfff;
   phase(0);
@@ -2516,7 +2535,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
     if (item >= nwork) break;
     uint32_t w = 0;
     work_item(b, s_cnt, 0, kNumLargeCls, item, &w);
-    blob_item<NT, CAP>(b, g, prm, S, gpk, s_combo, w, pacc);
+    blob_item<NT, CAP>(b, g, prm, S, gpk, s_combo, w, load_pair_info(b, w), pacc);
   }
   __syncthreads();
   probe_flush(b, prm, pacc, 80, tid == 0);
@@ -2546,11 +2565,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   // static round-robin over the size-ordered list: no dequeue atomic (a
   // device-scope atomic on one hot address is serviced at the memory side; one
   // per small blob serialized every wave of the chip behind that address)
+  // software pipeline over the wave's items: the work entry two items ahead and
+  // the pair-table entries one item ahead are in flight while a blob is processed
   const uint32_t nwaves = gridDim.x * 4;
-  for (uint32_t item = blockIdx.x * 4 + wave; item < nwork; item += nwaves) {
-    uint32_t w = 0;
+  uint32_t item = blockIdx.x * 4 + wave;
+  uint32_t w = 0, w1 = 0;
+  PairInfo pi = {0, 0, 0};
+  if (item < nwork) {
     work_item(b, s_cnt, kNumLargeCls, kNumCls, item, &w);
-    blob_item<64, kSmallBlob>(b, g, prm, S, nullptr, s_combo, w, pacc);
+    pi = load_pair_info(b, w);
+  }
+  if (item + nwaves < nwork) work_item(b, s_cnt, kNumLargeCls, kNumCls, item + nwaves, &w1);
+  for (; item < nwork; item += nwaves) {
+    const bool has1 = item + nwaves < nwork;
+    const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
+    uint32_t w2 = 0;
+    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, kNumLargeCls, kNumCls, item + 2 * nwaves, &w2);
+    blob_item<64, kSmallBlob>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
+    w = w1;
+    pi = pi1;
+    w1 = w2;
   }
   probe_flush(b, prm, pacc, 64, lane == 0);
   probe_flush_slow(b, prm, S, lane == 0);
@@ -2608,14 +2642,25 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
   __shared__ DecodeShared<RCAP> S;
   const int tid = threadIdx.x;
   // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
+  // (all lanes load the counts at once, B <= 256 = 4 per lane; wave scan)
   uint32_t* qpre = S.qpre;
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int f = 0; f < B; f++) {
-      qpre[f] = acc;
-      acc += min(b.nqcand[f], (uint32_t)kQuadCandPerFrame);
+  {
+    uint32_t c[kMaxBatch / 64], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxBatch / 64; k++) {
+      const int f = tid * (kMaxBatch / 64) + k;
+      c[k] = f < B ? min(b.nqcand[f], (uint32_t)kQuadCandPerFrame) : 0u;
+      sum += c[k];
     }
-    qpre[B] = acc;
+    const uint32_t incl = wave_incl_scan(sum, AddOp(), 0u);
+    uint32_t acc = incl - sum;
+#pragma unroll
+    for (int k = 0; k < kMaxBatch / 64; k++) {
+      const int f = tid * (kMaxBatch / 64) + k;
+      if (f < B) qpre[f] = acc;
+      acc += c[k];
+    }
+    if (tid == 63) qpre[B] = incl;
   }
   __syncthreads();
   const uint32_t nq = qpre[B];
@@ -2632,7 +2677,28 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       t_last = now;
     }
   };
-  for (uint32_t item = blockIdx.x; item < nq; item += gridDim.x) {  // static round-robin
+  // static round-robin over the queue in chunks of 64 items: one load per lane
+  // finds the chunk's accepted quads (rejected ones keep an invalid slot), so a
+  // run of rejected entries costs one round trip, not one each
+  const uint32_t G = gridDim.x;
+  for (uint32_t base = blockIdx.x; base < nq; base += 64u * G) {
+  uint64_t vmask;
+  {
+    const uint32_t it = base + (uint32_t)tid * G;
+    bool v = false;
+    if (it < nq) {
+      int lo = 0, hi = B - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (qpre[mid] <= it) lo = mid;
+        else hi = mid - 1;
+      }
+      v = b.qcand[(size_t)lo * kQuadCandPerFrame + (it - qpre[lo])].frame != kQuadInvalid;
+    }
+    vmask = __ballot(v);
+  }
+  for (; vmask; vmask &= vmask - 1) {
+    const uint32_t item = base + (uint32_t)__builtin_ctzll(vmask) * G;
     int lo = 0, hi = B - 1;  // last frame whose prefix <= item
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -2640,6 +2706,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       else hi = mid - 1;
     }
     const QuadCand& qd = b.qcand[(size_t)lo * kQuadCandPerFrame + (item - qpre[lo])];
+    if (qd.frame == kQuadInvalid) continue;  // a kept blob whose quad UpdateFitQuads rejected (uniform)
     const int f = (int)qd.frame;
     const uint32_t qrank = qd.rank;
     const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
@@ -2932,7 +2999,63 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     __syncthreads();
     phase(9);
   }
+  }
   probe_flush(b, prm, pacc, 128, tid == 0);
+}
+
+// ---------------------------------------------------------------------------
+// AT_STAGE_SIZES parity tap (debug copy only): the dense size plane the oracle
+// keeps (size[label] = pixels of the component, 0 elsewhere) from the forest:
+// entry i is the component size when i is a node id (fg (2r, 2c), bg (2r+1, 2c)
+// and (2r+1, 2c+1)) that is its own root and has pixels of its type in its block;
+// every other entry is 0 (k_thr_ccl writes sizes at such roots only).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint32_t* size,
+                                                   uint32_t* out, int Wd, int Hd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Wd * Hd) return;
+  const int y = i / Wd, x = i % Wd;
+  const int F = (y & ~1) * Wd + (x & ~1);
+  uint32_t v = 0;
+  bool node = true, has = false;
+  if ((y & 1) == 0) {
+    if (x & 1) node = false;  // (2r, 2c+1) is not a node
+    else has = thr[F] == 255 || thr[F + 1] == 255 || (y + 1 < Hd && (thr[F + Wd] == 255 || thr[F + Wd + 1] == 255));
+  } else {
+    has = thr[i] == 0 || thr[i - Wd] == 0;  // the block's column of this bg node
+  }
+  if (node && has && par[i] == (uint32_t)i) v = size[i];
+  out[i] = v;
+}
+
+// AT_STAGE_LABELS parity tap (debug copy only): LabelImage's output
+// (labeling_allegretti_2019_BKE.cu:340-462) from the forest: label =
+// par[par[node]] (node -> local root -> component root), 127 -> 0, a block of
+// four 127 pixels -> the pixel index.
+__global__ __launch_bounds__(256) void k_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd,
+                                                    int Hd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Wd * Hd) return;
+  const int y = i / Wd, x = i % Wd;
+  const int F = (y & ~1) * Wd + (x & ~1);
+  const bool all127 = thr[F] == 127 && thr[F + 1] == 127 && thr[F + Wd] == 127 && thr[F + Wd + 1] == 127;
+  uint32_t lab;
+  if (all127) lab = (uint32_t)i;
+  else if (thr[i] == 127) lab = 0;
+  else lab = par[par[thr[i] == 255 ? F : F + Wd + (x & 1)]];
+  out[i] = lab;
+}
+
+hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_tap_labels, dim3((Wd * Hd + 255) / 256), dim3(256), 0, st, thr, par, out, Wd, Hd);
+  return hipGetLastError();
+}
+
+hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint32_t* size, uint32_t* out, int Wd,
+                            int Hd, hipStream_t st) {
+  hipLaunchKernelGGL(k_tap_sizes, dim3((Wd * Hd + 255) / 256), dim3(256), 0, st, thr, par, size, out, Wd, Hd);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -3021,7 +3144,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     dim3 grd(g.CTX, g.CTY, B);
     tk(1, st, 0);
-    hipLaunchKernelGGL(k_thr_ccl, grd, dim3(256), 0, st, b, g, prm);
+    hipLaunchKernelGGL(k_thr_ccl, grd, dim3(kCclThreads), 0, st, b, g, prm);
     tk(1, st, 1);
     mark();
     tk(2, st, 0);
