@@ -201,7 +201,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.W = W; g.H = H; g.Wd = W / 2; g.Hd = H / 2;
   g.TW = g.Wd / 4; g.TH = g.Hd / 4;
   g.BW = g.Wd / 2; g.BH = g.Hd / 2;
-  g.CTX = (g.Wd + kCclTileW - 1) / kCclTileW;
+  g.ctw = d->B < kWideBlobMaxBatch ? 32 : 64;
+  if (getenv("AT_CCL_TILE")) g.ctw = atoi(getenv("AT_CCL_TILE")) == 32 ? 32 : 64;
+  g.CTX = (g.Wd + g.ctw - 1) / g.ctw;
   g.CTY = (g.Hd + kCclTileH - 1) / kCclTileH;
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
   g.BTX = (g.Wd - 2 + 63) / 64;
@@ -226,6 +228,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
   p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
   p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
+  p.pipe_stop = getenv("AT_DIAG_PIPE_STOP") ? atoi(getenv("AT_DIAG_PIPE_STOP")) : 0;
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {
     at_destroy(d);
@@ -282,7 +285,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.mm = (uint8_t*)dalloc(B * nt);
   b.thr = (uint8_t*)dalloc(B * nd);
   b.par = (uint32_t*)dalloc(B * nd * 4);
-  b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodes * 4);
+  b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodesMax * 4);
   b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
@@ -326,6 +329,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)
   b.s_pk = (uint64_t*)dalloc((size_t)d->nblobwg * (kSortCap / 2) * 8);
+  b.rsamp = (double*)dalloc((size_t)d->nblobwg * kDecodeGridPerBlobWg * 2 * (kMaxRefineSamples - kLdsRefine) * 8);
   if (oom) return fail(AT_E_NOMEM);
   // frame pointer table: fine-grained mapped host memory read by k_pre directly
   // (no host-to-device copy per batch; the GPU does not cache it)

@@ -9,14 +9,22 @@
 namespace at {
 
 // ---- capacities -----------------------------------------------------------
-// CCL tile: 64 x 32 decimated pixels = 32 x 16 2x2-blocks per 512-thread workgroup
-// (one thread per block): twice the pixels per workgroup of a 32 x 32 tile for the
-// same dependent round trips, and a third fewer tile-border unions per pixel
-constexpr int kCclTileW = 64;
+// CCL tile: TW x 32 decimated pixels = TW/2 x 16 2x2-blocks per workgroup (one thread
+// per block).  Throughput mode (max_batch >= kWideBlobMaxBatch) uses 64-wide tiles:
+// twice the pixels per workgroup of a 32-wide tile for the same dependent round
+// trips and a third fewer tile-border unions per pixel.  Latency mode (small
+// batches, few workgroups per frame) uses 32-wide tiles: twice the workgroups,
+// each with half the serial chain.
+template <int TW>
+struct CclTile {
+  static constexpr int W = TW, H = 32;
+  static constexpr int BW = TW / 2, BH = H / 2;  // blocks per tile row / column
+  static constexpr int NT = BW * BH;            // threads per workgroup
+  static constexpr int NODES = 3 * NT;          // union-find nodes of one tile
+  static constexpr int ROW_NODES = 3 * BW;      // node slots per block row
+};
 constexpr int kCclTileH = 32;
-constexpr int kCclBW = kCclTileW / 2, kCclBH = kCclTileH / 2;  // blocks per tile row / column
-constexpr int kCclThreads = kCclBW * kCclBH;                  // 512
-constexpr int kCclTileNodes = 3 * kCclThreads;                 // union-find nodes of one CCL tile
+constexpr int kCclTileNodesMax = CclTile<64>::NODES;  // stride of the per-tile local-root lists
 // per-frame open-addressing table of blob pairs: 4096 slots hold every frame the
 // 12-bit blob index admits (<= kMaxPairs keys; typical frames fill ~10 %), and keep
 // k_pairs' LDS copy at 84 KB so it co-resides with other kernels' workgroups
@@ -39,6 +47,11 @@ constexpr int kBlobThreads = 256;
 constexpr int kWideBlobMaxBatch = 8;
 constexpr int kSmallBlob = 512;        // blobs up to this many points go one-wave-per-blob
 constexpr int kNMaxima = 10;
+// RefineEdges samples of one quad (<= perimeter / 8 + 64, k_decode): the first
+// kLdsRefine in LDS, the rest in the decode workgroup's global scratch
+constexpr int kMaxRefineSamples = 1536;
+constexpr int kLdsRefine = 256;
+constexpr int kDecodeGridPerBlobWg = 8;  // k_decode workgroups <= nblobwg * this
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
 constexpr int kNumStages = 12;
@@ -72,6 +85,7 @@ struct Geom {
   int TW, TH;           // 4x4 threshold tiles
   int BW, BH;           // 2x2 CCL blocks
   int CTX, CTY;         // CCL tiles
+  int ctw;              // CCL tile width (32: latency mode, 64: throughput mode)
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)
   int BTX, BTY, ntb;    // k_boundary tiles (64 x 4*kBndRows interior pixels each)
   uint32_t min_cluster; // max(24, min_cluster_pixels)
@@ -91,6 +105,7 @@ struct Params {
   int probe;      // diagnostics only (AT_PHASE_PROBE): kernels stamp phase clocks into DevBufs::probe
   int taps;       // write the sorted IndexPoint parity tap (AT_STAGE_BLOB_POINTS) over the grouped points
   int wide_blob;  // AT_WIDE_BLOB=1: 512-thread large-blob teams at every batch size (experiment)
+  int pipe_stop;  // diagnostics only (AT_DIAG_PIPE_STOP): launch the stages < N only; 0 = all
 };
 constexpr int kProbeWords = 256;
 
@@ -142,7 +157,7 @@ struct DevBufs {
   uint8_t* mm;        // [B][TW*TH*2]   unfiltered 4x4 min/max
   uint8_t* thr;       // [B][Wd*Hd]
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
-  uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodes] local roots of each CCL tile (global node ids)
+  uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodesMax] local roots of each CCL tile (global node ids)
   uint32_t* nlroot;   // [B][CTX*CTY]
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
@@ -189,6 +204,7 @@ struct DevBufs {
   uint32_t* qhead;    // [1]
   QuadCand* qcand;    // [qcand_cap]
   uint32_t qcand_cap;
+  double* rsamp;      // [decode workgroups][2][kMaxRefineSamples - kLdsRefine] refine samples past LDS
   // per-workgroup scratch of the blob kernel
   uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
                       // (pathological blobs only; every other per-blob array lives in LDS)

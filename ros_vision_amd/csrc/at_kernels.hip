@@ -242,11 +242,15 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
 __device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// find with path halving: every visited node is pointed at its grandparent (an
+// ancestor with a smaller id, so the atomicMin never loses a link)
 __device__ __forceinline__ uint32_t lds_find(uint32_t* par, uint32_t n) {
   uint32_t p = lds_load(par + n);
   while (p != n) {
+    const uint32_t gp = lds_load(par + p);
+    if (gp != p) atomicMin(&par[n], gp);
     n = p;
-    p = lds_load(par + n);
+    p = gp;
   }
   return n;
 }
@@ -268,13 +272,17 @@ __device__ __forceinline__ void lds_union(uint32_t* par, uint32_t a, uint32_t b)
   }
 }
 
-constexpr int kCclRowNodes = 3 * kCclBW;  // node slots per block row
+template <int TW>
 __device__ __forceinline__ uint32_t slot_of(int ty, int tx, int type) {
-  return (uint32_t)(ty * kCclRowNodes + (type == 0 ? tx : kCclBW + 2 * tx + (type - 1)));
+  using T = CclTile<TW>;
+  return (uint32_t)(ty * T::ROW_NODES + (type == 0 ? tx : T::BW + 2 * tx + (type - 1)));
 }
 
-__global__ __launch_bounds__(kCclThreads) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
-  constexpr int NT = kCclThreads;
+template <int TWD>
+__global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
+  using CT = CclTile<TWD>;
+  constexpr int NT = CT::NT;
+  constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES, kCclRowNodes = CT::ROW_NODES;
   constexpr int kTW = kCclTileW / 4, kTH = kCclTileH / 4;  // 4x4 threshold tiles per CCL tile
   constexpr int kHR = kCclTileH + 1, kHC = kCclTileW + 2;  // threshold halo: rows y0-1.., cols x0-1..x0+W
   const int f = blockIdx.z;
@@ -353,10 +361,7 @@ __global__ __launch_bounds__(kCclThreads) void k_thr_ccl(DevBufs b, Geom g, Para
       s_t[r][c] = res;
     }
   }
-  for (int i = tid; i < kCclTileNodes; i += NT) {
-    s_par[i] = i;
-    s_cnt[i] = 0;
-  }
+  for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
   __syncthreads();
   // write this tile's threshold plane (4 bytes per thread)
   {
@@ -368,27 +373,63 @@ __global__ __launch_bounds__(kCclThreads) void k_thr_ccl(DevBufs b, Geom g, Para
       *reinterpret_cast<uint32_t*>(thr + (size_t)y * g.Wd + x) = w;
     }
   }
-  // local unions over intra-tile edges (InitLabeling P/Q/R/S + Merge)
+  // Local labeling (InitLabeling P/Q/R/S + Merge, labeling_allegretti_2019_BKE.cu:114-338)
+  // in two steps.  (1) Horizontal runs without atomics: within a block row the
+  // fg nodes form a chain (F(x-1) - F(x)) and the bg nodes another
+  // (... R(x-1) - L(x) - R(x) - L(x+1) ...); a wave holds whole block rows, so
+  // every node finds its run head -- the leftmost node, i.e. the smallest id --
+  // from two ballots.  (2) Vertical links (up-left, up, up-right for fg; up for
+  // bg) as union-find unions on the run heads, a run linking to each run above
+  // it once (a block skips a target its left neighbour in the same run links to).
   const int bty = tid / kCclBW, btx = tid % kCclBW;
 #define T(rr, cc) s_t[(rr) + 1][(cc) + 1]
   const int pr = 2 * bty, pc = 2 * btx;
   const uint8_t a = T(pr, pc), bb = T(pr, pc + 1), c = T(pr + 1, pc), d = T(pr + 1, pc + 1);
-  const uint32_t F = slot_of(bty, btx, 0), L = slot_of(bty, btx, 1), R = slot_of(bty, btx, 2);
-  if (bty > 0) {
-    if (btx > 0 && a == 255 && T(pr - 1, pc - 1) == 255) lds_union(s_par, F, slot_of(bty - 1, btx - 1, 0));
-    if ((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255))
-      lds_union(s_par, F, slot_of(bty - 1, btx, 0));
-    if (btx < kCclBW - 1 && bb == 255 && T(pr - 1, pc + 2) == 255) lds_union(s_par, F, slot_of(bty - 1, btx + 1, 0));
-    if (a == 0 && T(pr - 1, pc) == 0) lds_union(s_par, L, slot_of(bty - 1, btx, 1));
-    if (bb == 0 && T(pr - 1, pc + 1) == 0) lds_union(s_par, R, slot_of(bty - 1, btx, 2));
+  const uint32_t F = slot_of<TWD>(bty, btx, 0), L = slot_of<TWD>(bty, btx, 1), R = slot_of<TWD>(bty, btx, 2);
+  const uint32_t lane = lane_id();
+  {
+    const bool fg_left = btx > 0 && (a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255);
+    const bool bg_left = btx > 0 && ((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0));
+    const bool bg_in = (a == 0 && bb == 0) || (c == 0 && d == 0);  // R(x) - L(x)
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
+    const uint64_t lt = (1ull << lane) - 1;                          // lanes < this one
+    const uint64_t fs = __ballot(!fg_left);  // run starts (btx == 0 always starts: rows never merge)
+    const int hf = 63 - __builtin_clzll(fs & le);
+    const uint32_t hF = F - (uint32_t)(lane - hf);
+    const uint64_t sl = __ballot(!bg_left), sr = __ballot(!bg_in);
+    uint32_t hL, hR;
+    if (!bg_left) {
+      hL = L;
+    } else {  // last run start before L(x): in the nearest lane below with a start, its R if R starts there
+      const int hl = 63 - __builtin_clzll((sl | sr) & lt);
+      hL = ((sr >> hl) & 1) ? slot_of<TWD>(bty, btx - (lane - hl), 2) : slot_of<TWD>(bty, btx - (lane - hl), 1);
+    }
+    hR = bg_in ? hL : R;
+    s_par[F] = hF;
+    s_par[L] = hL;
+    s_par[R] = hR;
+    __syncthreads();
+    // heads of the run(s) above this block's vertical links (read before any union)
+    constexpr uint32_t kNone = 0xffffffffu;
+    uint32_t tUL = kNone, tU = kNone, tUR = kNone, tL = kNone, tR = kNone;
+    if (bty > 0) {
+      if (btx > 0 && a == 255 && T(pr - 1, pc - 1) == 255) tUL = s_par[slot_of<TWD>(bty - 1, btx - 1, 0)];
+      if ((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255))
+        tU = s_par[slot_of<TWD>(bty - 1, btx, 0)];
+      if (btx < kCclBW - 1 && bb == 255 && T(pr - 1, pc + 2) == 255) tUR = s_par[slot_of<TWD>(bty - 1, btx + 1, 0)];
+      if (a == 0 && T(pr - 1, pc) == 0) tL = s_par[slot_of<TWD>(bty - 1, btx, 1)];
+      if (bb == 0 && T(pr - 1, pc + 1) == 0) tR = s_par[slot_of<TWD>(bty - 1, btx, 2)];
+    }
+    // the left neighbour's targets (same wave: rows never straddle waves)
+    const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
+    __syncthreads();
+    auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
+    if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
+    if (tU != kNone && tU != tUL && !seen_fg(tU)) lds_union(s_par, hF, tU);
+    if (tUR != kNone && tUR != tUL && tUR != tU && !seen_fg(tUR)) lds_union(s_par, hF, tUR);
+    if (tL != kNone && !(bg_left && tL == pR)) lds_union(s_par, hL, tL);
+    if (tR != kNone && !(bg_in && tR == tL)) lds_union(s_par, hR, tR);
   }
-  if (btx > 0) {
-    if ((a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255))
-      lds_union(s_par, F, slot_of(bty, btx - 1, 0));
-    if ((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0))
-      lds_union(s_par, L, slot_of(bty, btx - 1, 2));
-  }
-  if ((a == 0 && bb == 0) || (c == 0 && d == 0)) lds_union(s_par, R, L);
 #undef T
   __syncthreads();
   const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
@@ -430,7 +471,7 @@ __global__ __launch_bounds__(kCclThreads) void k_thr_ccl(DevBufs b, Geom g, Para
     }
     // the tile's local roots (components with pixels), for k_ccl_roots
     const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
-    uint32_t* lr = b.lroot + tl * kCclTileNodes;
+    uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
     if (cF) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
     if (cL) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
     if (cR) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
@@ -503,9 +544,16 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
 // P, Q, R and the two background links), then the left block column (BH x P, S,
 // background S), then the right column (BH-1 x R).  Every union is one short
 // chain of global round trips instead of up to five in a row per lane.
-constexpr int kBorderTop = 5 * kCclBW, kBorderLeft = 3 * kCclBH, kBorderRight = kCclBH - 1;
-constexpr int kBorderThreads = (kBorderTop + kBorderLeft + kBorderRight + 63) / 64 * 64;
-__global__ __launch_bounds__(kBorderThreads) void k_ccl_border(DevBufs b, Geom g) {
+template <int TW>
+struct BorderRoles {
+  static constexpr int Top = 5 * CclTile<TW>::BW, Left = 3 * CclTile<TW>::BH, Right = CclTile<TW>::BH - 1;
+  static constexpr int NT = (Top + Left + Right + 63) / 64 * 64;
+};
+template <int TWD>
+__global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, Geom g) {
+  constexpr int kBorderTop = BorderRoles<TWD>::Top, kBorderLeft = BorderRoles<TWD>::Left,
+                kBorderRight = BorderRoles<TWD>::Right;
+  constexpr int kCclBW = CclTile<TWD>::BW, kCclBH = CclTile<TWD>::BH;
   const int f = blockIdx.z;
   const int t = threadIdx.x;
   int bty, btx, role, kind;
@@ -568,7 +616,7 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   uint32_t* par = b.par + fo;
   uint32_t* size = b.size + fo;
   const uint32_t n = b.nlroot[tl];
-  const uint32_t* lr = b.lroot + tl * kCclTileNodes;
+  const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
   for (uint32_t k = threadIdx.x; k < n; k += 64) {
     const uint32_t l = lr[k];
     const uint32_t r = g_find(par, l);
@@ -2609,17 +2657,12 @@ __constant__ double c_rot_c[4] = {1.0, 6.123233995736766e-17, -1.0, -1.836970198
 __constant__ double c_rot_s[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
 // Refine samples of one quad: 4 edges of max(16, len / 8) samples, so at most
 // perimeter / 8 + 64 for a quad inside the frame (perimeter <= 2 (W + H)).  The
-// LDS sample buffer is sized by the geometry (768 covers 720p, 1024 1080p,
-// 1536 every frame the reference admits): a 17 KB workgroup instead of 29 KB
-// keeps 8 quads per CU in flight.
-constexpr int kMaxRefineSamples = 1536;
-__host__ __device__ constexpr int refine_cap_for(int W, int H) {
-  return (2 * (W + H) + 7) / 8 + 64 <= 768 ? 768 : ((2 * (W + H) + 7) / 8 + 64 <= 1024 ? 1024 : kMaxRefineSamples);
-}
+// first kLdsRefine samples (every quad of side <= ~380 px) live in LDS, the rest
+// of a huge quad in the workgroup's global scratch (DevBufs::rsamp): an 8.5 KB
+// workgroup instead of 17 KB doubles the quads in flight per CU.
 
-template <int RCAP>
 struct DecodeShared {
-  double sx[RCAP], sy[RCAP];
+  double sx[kLdsRefine], sy[kLdsRefine];
   float qc[4][2];
   int nsamp[4], samp_off[4];
   float enx[4], eny[4];
@@ -2637,10 +2680,12 @@ struct DecodeShared {
   uint32_t qpre[kMaxBatch + 1];
 };
 
-template <int RCAP>
 __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm, int B) {
-  __shared__ DecodeShared<RCAP> S;
+  constexpr int RCAP = kMaxRefineSamples;
+  __shared__ DecodeShared S;
   const int tid = threadIdx.x;
+  double* gsx = b.rsamp + (size_t)blockIdx.x * (2 * (kMaxRefineSamples - kLdsRefine));
+  double* gsy = gsx + (kMaxRefineSamples - kLdsRefine);
   // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
   // (all lanes load the counts at once, B <= 256 = 4 per lane; wave scan)
   uint32_t* qpre = S.qpre;
@@ -2780,8 +2825,13 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
           by = y0 + n0 * ny;
           undistort(prm, &bx, &by);
         }
-        S.sx[t] = bx;
-        S.sy[t] = by;
+        if (t < kLdsRefine) {
+          S.sx[t] = bx;
+          S.sy[t] = by;
+        } else {
+          gsx[t - kLdsRefine] = bx;
+          gsy[t - kLdsRefine] = by;
+        }
       }
       __syncthreads();
       phase(1);
@@ -2789,7 +2839,9 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
         double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
         const int o = S.samp_off[tid];
         for (int s = 0; s < S.nsamp[tid] && o + s < RCAP; s++) {
-          const double bx = S.sx[o + s], by = S.sy[o + s];
+          const int i = o + s;
+          const double bx = i < kLdsRefine ? S.sx[i] : gsx[i - kLdsRefine];
+          const double by = i < kLdsRefine ? S.sy[i] : gsy[i - kLdsRefine];
           if (isnan(bx)) continue;
           Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
         }
@@ -3118,6 +3170,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt) {
   int e = 0;
+  auto on = [&](int stage) { return prm.pipe_stop <= 0 || stage < prm.pipe_stop; };
   auto mark = [&]() {
     if (ev) (void)hipEventRecord(ev[e++], st);
   };
@@ -3135,7 +3188,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     dim3 blk(64, 4), grd((g.TW + 63) / 64, (g.TH + 3) / 4, B);
     tk(0, st, 0);
-    if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
+    if (!on(0)) {}
+    else if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
     else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
     else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
     tk(0, st, 1);
@@ -3144,41 +3198,46 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     dim3 grd(g.CTX, g.CTY, B);
     tk(1, st, 0);
-    hipLaunchKernelGGL(k_thr_ccl, grd, dim3(kCclThreads), 0, st, b, g, prm);
+    if (!on(1)) {}
+    else if (g.ctw == 32) hipLaunchKernelGGL(k_thr_ccl<32>, grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
+    else hipLaunchKernelGGL(k_thr_ccl<64>, grd, dim3(CclTile<64>::NT), 0, st, b, g, prm);
     tk(1, st, 1);
     mark();
     tk(2, st, 0);
-    hipLaunchKernelGGL(k_ccl_border, grd, dim3(kBorderThreads), 0, st, b, g);
+    if (!on(2)) {}
+    else if (g.ctw == 32) hipLaunchKernelGGL(k_ccl_border<32>, grd, dim3(BorderRoles<32>::NT), 0, st, b, g);
+    else hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
     tk(2, st, 1);
     mark();
   }
   tk(3, st, 0);
-  hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+  if (on(3)) hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
   tk(3, st, 1);
   mark();
   {
     dim3 blk(64, 4), grd(g.BTX, g.BTY, B);
     tk(4, st, 0);
-    hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
+    if (on(4)) hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
     tk(4, st, 1);
     mark();
   }
   tk(5, st, 0);
-  hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
+  if (on(5)) hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
   tk(5, st, 1);
   mark();
   tk(6, st, 0);
-  hipLaunchKernelGGL(k_group, dim3(g.ntb, B), dim3(256), 0, st, b, g);
+  if (on(6)) hipLaunchKernelGGL(k_group, dim3(g.ntb, B), dim3(256), 0, st, b, g);
   tk(6, st, 1);
   mark();
   tk(7, st, 0);
-  hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
+  if (on(7)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
   tk(7, st, 1);
   mark();
   auto blob_large = [&](hipStream_t s) {
     tk(9, s, 0);
     // LDS sized for the largest blob the geometry admits (max_cluster = 2 (W + H))
     const bool cap4k = g.max_cluster <= 4096;
+    if (!on(9)) return;
     if (B < kWideBlobMaxBatch || prm.wide_blob) {
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
@@ -3190,7 +3249,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   };
   auto blob_small = [&](hipStream_t s) {
     tk(8, s, 0);
-    hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    if (on(8)) hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
     tk(8, s, 1);
   };
   if (ev || !st2) {
@@ -3210,17 +3269,14 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(10, st, 0);
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups
-    // for every quad of a full batch to start at once (8 per CU at 17 KB LDS)
-    const dim3 grd(std::max(nblobwg * 2, std::min(nblobwg * 4, 64 * B)));
-    const int rcap = refine_cap_for(g.W, g.H);
-    if (rcap == 768) hipLaunchKernelGGL(k_decode<768>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
-    else if (rcap == 1024) hipLaunchKernelGGL(k_decode<1024>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
-    else hipLaunchKernelGGL(k_decode<kMaxRefineSamples>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+    // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
+    const dim3 grd(std::max(nblobwg * 2, std::min(nblobwg * kDecodeGridPerBlobWg, 64 * B)));
+    if (on(10)) hipLaunchKernelGGL(k_decode, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
   }
   tk(10, st, 1);
   mark();
   tk(11, st, 0);
-  if (prm.tag_size > 0)
+  if (prm.tag_size > 0 && on(11))
     hipLaunchKernelGGL(k_pose, dim3(kPoseGroupsPerFrame, B), dim3(64), 0, st, b, prm);
   tk(11, st, 1);
   mark();

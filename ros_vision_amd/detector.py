@@ -16,7 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libat_hip.so")
+# AT_HIP_LIB overrides the library (A/B timing of build variants, tools/ab.sh)
+LIB_PATH = os.environ.get("AT_HIP_LIB") or os.path.join(_HERE, "libat_hip.so")
 
 AT_FMT_YUYV, AT_FMT_BGR8, AT_FMT_GRAY8 = 0, 1, 2
 (AT_STAGE_GRAY, AT_STAGE_DECIMATED, AT_STAGE_THRESHOLD, AT_STAGE_LABELS, AT_STAGE_SIZES,
