@@ -306,12 +306,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host0 = [d.batch_stats() for d in dets]
     ndet = run(args.steps, step0=args.warmup)
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    host1 = [d.batch_stats() for d in dets]
     kt = [d.kernel_time() for d in dets] if ktimer else [(0.0, 0)]
     k_launches = sum(n for _, n in kt)
     k_ms = sum(ms * n for ms, n in kt) / max(1, k_launches)
@@ -407,6 +409,8 @@ def main():
                               "bytes_per_frame": pipe_bytes,
                               "note": "SURVEY.md 8(d): per-GPU frames/s x 3*W*H; traffic = PMC bytes per frame"},
         "batch_stats": stats,
+        "host_us_per_step": {k: round(sum(b[k] - a[k] for a, b in zip(host0, host1)) / args.steps, 1)
+                             for k in ("host_wait_us_total", "host_tail_us_total")},
         "stage_ms_per_batch": {k: round(v, 4) for k, v in stages.items()},
         "dominant_kernel": dominant,
         "pipeline_gpu_ms_per_batch": round(pipe_ms, 4) if pipe_ms else None,

@@ -162,7 +162,9 @@ int at_kernel_time(at_detector *d, double *avg_ms, long long *launches);
 
 /* Work counts of the last collected batch: [0] frames, [1] boundary points,
  * [2] blob pairs, [3] points processed by the small-blob kernel, [4] by the
- * large-blob kernel, [5] fitted quads, [6] decoded candidates (pre-reconcile).
+ * large-blob kernel, [5] fitted quads, [6] decoded candidates (pre-reconcile);
+ * host time of this detector since creation, microseconds: [7] waiting in
+ * at_collect for the GPU, [8] in the host tail (reconcile, sort, poses).
  * Returns the number of entries written. */
 int at_batch_stats(at_detector *d, uint64_t *out, int cap);
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -88,6 +89,7 @@ struct at_detector {
   hipEvent_t ev_stage[kNumStages + 1];
   double stage_ms[kNumStages];
   long stage_batches;
+  double host_wait_us, host_tail_us;  // cumulative time of at_collect in the event wait / the host tail
 };
 
 static int hip_fail(hipError_t e) {
@@ -554,9 +556,16 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   return AT_OK;
 }
 
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_per_frame) {
   if (!d->pending) return AT_E_INVALID;
+  const double t0 = now_us();
   HIPCHK(hipEventSynchronize(d->ev_done));
+  const double t1 = now_us();
+  d->host_wait_us += t1 - t0;
   d->pending = 0;
   if (d->profiling) {
     for (int i = 0; i < kNumStages; i++) {
@@ -587,6 +596,7 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
     d->nposes[f] = d->prm.tag_size > 0 ? std::min(n, kMaxDets) : 0;
     if (n_per_frame) n_per_frame[f] = n;
   }
+  d->host_tail_us += now_us() - t1;
   return rc;
 }
 
@@ -706,7 +716,10 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   v[5] = d->h_ctrl[kCtlNquads * B];  // FitQuads records of the batch (counted per blob team)
   v[3] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts];
   v[4] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts + 1];
-  const int n = std::min(cap, 7);
+  v[7] = (uint64_t)d->host_wait_us;
+  uint64_t tail = (uint64_t)d->host_tail_us;
+  const int n = std::min(cap, 9);
+  if (n > 8) out[8] = tail;
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
 }

@@ -1475,26 +1475,24 @@ __device__ __forceinline__ float window_err(const Mom6& s, int32_t N) {
 // u32 compact point words in bytes [0, 4n) and f32 window errors in bytes
 // [4 CAP, 4 CAP + 4n).  The union holds, in turn, the bucket-sort counts, the
 // peak keys and the 90 segment fits of FitQuads.
-template <int CAP>
-constexpr int kPeakCap = (CAP / 4 * 4 > 3200 ? CAP / 4 * 4 : 3200) / 8;
 
 template <int NT, int CAP>
 constexpr int kKeySlots = (NT >= 512 && CAP <= 4096) ? 2 * CAP : CAP;  // latency-mode teams: bucket scatter room for CAP keys
 
+// the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
+// a > b wrap-around pi[a]->pi[b] (the closing side m3->m0).  They live over the
+// team's key area, which is dead by then (3.2 KB <= 8 CAP bytes).
+struct SegFits {
+  double err[kNMaxima][kNMaxima];
+  double mse[kNMaxima][kNMaxima];
+  double p[kNMaxima][kNMaxima][2];
+};
+
 template <int NT, int CAP>
 struct BlobShared {
   uint64_t keys[kKeySlots<NT, CAP>];
-  union {
-    uint32_t bcnt[kKeySlots<NT, CAP> / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
-    uint64_t peaks[kPeakCap<CAP>];
-    struct {
-      // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
-      // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0)
-      double err[kNMaxima][kNMaxima];
-      double mse[kNMaxima][kNMaxima];
-      double p[kNMaxima][kNMaxima][2];
-    } seg;
-  } u;
+  uint32_t bcnt[kKeySlots<NT, CAP> / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
+  uint64_t pks[16];                        // the top-10 peak keys (peaks themselves stay in registers)
   // inclusive prefix moments at the indices FitQuads reads: [k] = P[pi[k]],
   // [10 + k] = P[pi[k] - 1], [20] = P[n - 1]
   uint32_t tMx[21], tMy[21], tW[21];
@@ -1532,7 +1530,7 @@ __device__ bool team_bucket_sort(BlobShared<NT, CAP>& S, int n) {
   int nb = 32;
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n buckets, power of two, <= KEYS/2
   auto bucket = [&](uint64_t k) { return (uint32_t)(((k >> kKeyTheta) * (uint64_t)nb) / kThetaSpan); };
-  uint32_t* bcnt = S.u.bcnt;
+  uint32_t* bcnt = S.bcnt;
   for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
   team_sync<NT>();
   for (int t = tid; t < n; t += NT) {
@@ -1728,7 +1726,7 @@ __device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, in
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n, power of two, <= 256
   const int sh = 26 - __builtin_ctz((unsigned)nb);
   auto bucket = [&](uint64_t k) { return (uint32_t)((k >> kKeyTheta) >> sh); };
-  uint32_t* bcnt = S.u.bcnt;  // two u16 counters per word
+  uint32_t* bcnt = S.bcnt;  // two u16 counters per word
   for (int i = (int)lane; i < nb / 2; i += 64) bcnt[i] = 0;
   team_sync<64>();
 #pragma unroll
@@ -1835,7 +1833,7 @@ __device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp
   if (nb / 2 > KEYS / 4) return false;
   const int sh = 26 - __builtin_ctz((unsigned)nb);
   auto bucket = [&](uint64_t k) { return (uint32_t)((k >> kKeyTheta) >> sh); };
-  uint32_t* bcnt = S.u.bcnt;
+  uint32_t* bcnt = S.bcnt;
   for (int i = tid; i < nb / 2; i += NT) bcnt[i] = 0;
   team_sync<NT>();
 #pragma unroll
@@ -1954,8 +1952,6 @@ template <int NT, int CAP>
 __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S, uint64_t* gpk,
                           const uint32_t* combo, uint32_t w, PairInfo pi_, uint32_t* pacc) {
   constexpr int kC = (CAP + NT - 1) / NT;  // max points per thread chunk
-  constexpr int kPk = kPeakCap<CAP>;
-  constexpr bool kGlobPk = kPk < CAP / 2;  // peaks (<= n/2) may overflow the LDS area
   static_assert(kC <= 32, "chunk too long");
   const int tid = team_rank<NT>();
   const uint32_t lane = lane_id();
@@ -2083,12 +2079,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       errv[t] = window_err(s, Nw);
     }
   }
-  if (tid == 0) S.npeaks = 0;
   team_sync<NT>();
   phase(4);
 
   // ---- 7-tap filter and strict local maxima; peak keys (P8-P10: -filtered
-  // error in cub's float radix order, then point index)
+  // error in cub's float radix order, then point index).  Each thread keeps its
+  // chunk's peaks in registers: strict maxima are never adjacent, so chunk
+  // position k has slot k / 2 to itself
   auto filt_at = [&](uint32_t t) -> double {
     double acc = 0.0;
 #pragma unroll
@@ -2100,44 +2097,43 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     }
     return acc;
   };
-  uint64_t* pks = S.u.peaks;
+  constexpr int kPR = (kC + 1) / 2;
+  uint64_t mine[kPR];
+#pragma unroll
+  for (int j = 0; j < kPR; j++) mine[j] = ~0ull;
+  uint32_t nmine = 0;
   if (t0 < t1) {
     double fprev = filt_at(t0 == 0 ? n - 1 : t0 - 1), fcur = filt_at(t0);
-    for (uint32_t t = t0; t < t1; t++) {
+#pragma unroll
+    for (int k = 0; k < kC; k++) {
+      const uint32_t t = t0 + k;
+      if (k >= (int)c || t >= t1) break;
       const double fnext = filt_at(t + 1 == n ? 0 : t + 1);
       if (fcur > fprev && fcur > fnext) {
         const float ef = (float)(-fcur);
         uint32_t u = __float_as_uint(ef);
         u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // cub radix float order
-        const uint32_t slot = atomicAdd(&S.npeaks, 1u);
-        pk_put<kGlobPk>(pks, gpk, kPk, (int)slot, ((uint64_t)u << 32) | t);
+        mine[k >> 1] = ((uint64_t)u << 32) | t;
+        nmine++;
       }
       fprev = fcur;
       fcur = fnext;
     }
   }
-  team_sync<NT>();
-  const uint32_t npk = S.npeaks;
+  const uint32_t npk = team_reduce<NT>(nmine, AddOp(), S.red_u32);
+  uint64_t* pks = S.pks;
   {
     // FitQuads reads only the first min(10, npk) entries of the peak order (P9
     // sorts all of a blob's peaks): select them -- 10 rounds of a team minimum
     // over the keys (unique: the point index is in the low word) above the
     // previous pick -- instead of sorting every peak
-    constexpr int kPP = (CAP / 2 + NT - 1) / NT;  // a cyclic sequence of n has <= n/2 strict maxima
-    uint64_t mine[kPP];
-#pragma unroll
-    for (int j = 0; j < kPP; j++) {
-      const int t = j * NT + tid;
-      mine[j] = t < (int)npk ? pk_get<kGlobPk>(pks, gpk, kPk, t) : ~0ull;
-    }
     const int ntop = npk < (uint32_t)kNMaxima ? (int)npk : kNMaxima;
     uint64_t* red = reinterpret_cast<uint64_t*>(S.red_f64);
     uint64_t last = 0;
-    team_sync<NT>();  // every peak read before slots 0..9 are rewritten
     for (int r = 0; r < ntop; r++) {
       uint64_t m = ~0ull;
 #pragma unroll
-      for (int j = 0; j < kPP; j++) {
+      for (int j = 0; j < kPR; j++) {
         const uint64_t k = mine[j];
         if ((r == 0 || k > last) && k < m) m = k;
       }
@@ -2198,15 +2194,18 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     return to_moments(m, N);
   };
   // every segment a combination can use, fitted once (FitLine on the same
-  // moments as QuadFitCalculator's per-combination fits: identical results)
+  // moments as QuadFitCalculator's per-combination fits: identical results),
+  // over the key area (its compact words were last read by the prefix lookups)
+  SegFits& seg = *reinterpret_cast<SegFits*>(S.keys);
+  static_assert(sizeof(SegFits) <= sizeof(S.keys), "segment fits must fit over the keys");
   for (int ci = tid; cnt >= 4 && ci < kNMaxima * kNMaxima; ci += NT) {
     const int a = ci / kNMaxima, bb = ci % kNMaxima;
     if (a != bb && a < cnt && bb < cnt) {
       const LineFitOut o = fit_line_v<false, true>(seg_moments(a, bb));
-      S.u.seg.err[a][bb] = o.err;
-      S.u.seg.mse[a][bb] = o.mse;
-      S.u.seg.p[a][bb][0] = o.p23[0];
-      S.u.seg.p[a][bb][1] = o.p23[1];
+      seg.err[a][bb] = o.err;
+      seg.mse[a][bb] = o.mse;
+      seg.p[a][bb][0] = o.p23[0];
+      seg.p[a][bb][1] = o.p23[1];
     }
   }
   team_sync<NT>();
@@ -2221,13 +2220,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     if (cnt >= 4) {
       const uint32_t cb = combo[ci];  // LDS copy of c_combo: no vector-memory wait in this loop
       const int m0 = cb & 0xff, m1 = (cb >> 8) & 0xff, m2 = (cb >> 16) & 0xff, m3 = cb >> 24;
-      if (m3 < cnt && !(S.u.seg.mse[m0][m1] > mse_max)) {
-        if (!(S.u.seg.mse[m1][m2] > mse_max)) {
+      if (m3 < cnt && !(seg.mse[m0][m1] > mse_max)) {
+        if (!(seg.mse[m1][m2] > mse_max)) {
           const double dot =
-              S.u.seg.p[m0][m1][0] * S.u.seg.p[m1][m2][0] + S.u.seg.p[m0][m1][1] * S.u.seg.p[m1][m2][1];
+              seg.p[m0][m1][0] * seg.p[m1][m2][0] + seg.p[m0][m1][1] * seg.p[m1][m2][1];
           if (!(fabs(dot) > prm.cos_critical_rad)) {
-            if (!(S.u.seg.mse[m2][m3] > mse_max) && !(S.u.seg.mse[m3][m0] > mse_max))
-              e4 = S.u.seg.err[m0][m1] + S.u.seg.err[m1][m2] + S.u.seg.err[m2][m3] + S.u.seg.err[m3][m0];
+            if (!(seg.mse[m2][m3] > mse_max) && !(seg.mse[m3][m0] > mse_max))
+              e4 = seg.err[m0][m1] + seg.err[m1][m2] + seg.err[m2][m3] + seg.err[m3][m0];
           }
         }
       }
@@ -2595,8 +2594,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
 // waves per workgroup, persistent over the small work list.  Everything a blob
 // needs lives in its wave's LDS slice (no global scratch).
-static_assert(kPeakCap<kSmallBlob> >= kSmallBlob / 2, "small-blob peaks must fit in LDS");
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_blob_small(DevBufs b, Geom g, Params prm) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_blob_small(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<64, kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();

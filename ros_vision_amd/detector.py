@@ -381,12 +381,12 @@ class GpuDetector:
         return ms.value, n.value
 
     BATCH_STATS = ("frames", "boundary_points", "pairs", "small_blob_points", "large_blob_points",
-                   "quads", "candidates")
+                   "quads", "candidates", "host_wait_us_total", "host_tail_us_total")
 
     def batch_stats(self):
         """Work counts of the last collected batch (see at_batch_stats)."""
-        buf = (C.c_uint64 * 8)()
-        n = _check(load_library().at_batch_stats(self._h, buf, 8), "at_batch_stats")
+        buf = (C.c_uint64 * 9)()
+        n = _check(load_library().at_batch_stats(self._h, buf, 9), "at_batch_stats")
         return dict(zip(self.BATCH_STATS, [int(x) for x in buf[:n]]))
 
     def detections(self, frame=0):
