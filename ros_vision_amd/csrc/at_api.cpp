@@ -211,6 +211,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.BTX = (g.Wd - 2 + 63) / 64;
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
   g.ntb = g.BTX * g.BTY;
+  g.bnd_region = kBndPts;
+  if (getenv("AT_BND_REGION")) g.bnd_region = std::max(kBndStage, std::min(kBndPts, atoi(getenv("AT_BND_REGION"))));  // experiment
   if (g.ntb > kMaxTilesPerFrame) {
     at_destroy(d);
     return AT_E_INVALID;
@@ -291,7 +293,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
-  b.pts = (uint64_t*)dalloc(B * ntb * kBndPts * 8);
+  b.pts = (uint64_t*)dalloc(B * ntb * (size_t)g.bnd_region * 8);
   b.tcnt = (uint32_t*)dalloc(B * ntb * 4);
   b.tent = (uint32_t*)dalloc(B * ntb * 4);
   b.grp = (uint64_t*)dalloc(B * g.cap_pts * 8);
@@ -403,45 +405,54 @@ static int prefer_smaller(int pref, double q0, double q1) {
 }
 
 static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int cap, at_pose* poses) {
-  std::vector<DevDetection> v(cand, cand + ncand);
-  std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.blob_rank < b.blob_rank; });
-  int n = (int)v.size();
+  // the reference's zarray operations on an index array (the 272-byte records stay
+  // where k_decode / k_pose wrote them): order by blob rank, reconcile with the
+  // same swap-with-last removals, stable sort by id
+  thread_local std::vector<int> idx;
+  idx.resize((size_t)ncand);
+  for (int i = 0; i < ncand; i++) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cand[a].blob_rank < cand[b].blob_rank; });
+  int n = ncand;
   for (int i0 = 0; i0 < n; i0++) {
     for (int i1 = i0 + 1; i1 < n; i1++) {
-      if (v[i0].id != v[i1].id) continue;
-      if (!poly_overlap(v[i0].p, v[i1].p)) continue;
+      const DevDetection& a = cand[idx[i0]];
+      const DevDetection& b = cand[idx[i1]];
+      if (a.id != b.id) continue;
+      if (!poly_overlap(a.p, b.p)) continue;
       int pref = 0;
-      pref = prefer_smaller(pref, v[i0].hamming, v[i1].hamming);
-      pref = prefer_smaller(pref, -v[i0].decision_margin, -v[i1].decision_margin);
-      for (int k = 0; k < 3; k++) pref = prefer_smaller(pref, v[i0].H[k], v[i1].H[k]);
+      pref = prefer_smaller(pref, a.hamming, b.hamming);
+      pref = prefer_smaller(pref, -a.decision_margin, -b.decision_margin);
+      for (int k = 0; k < 3; k++) pref = prefer_smaller(pref, a.H[k], b.H[k]);
       if (pref < 0) {  // keep i0; zarray_remove_index(shuffle=1)
-        if (i1 < n - 1) v[i1] = v[n - 1];
+        if (i1 < n - 1) idx[i1] = idx[n - 1];
         n--;
         i1--;
       } else {
-        if (i0 < n - 1) v[i0] = v[n - 1];
+        if (i0 < n - 1) idx[i0] = idx[n - 1];
         n--;
         i0--;
         break;
       }
     }
   }
-  v.resize(n);
-  std::stable_sort(v.begin(), v.end(), [](const DevDetection& a, const DevDetection& b) { return a.id < b.id; });
+  idx.resize((size_t)n);
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cand[a].id < cand[b].id; });
   for (int i = 0; i < n && i < kMaxDets; i++) {
-    poses[i].id = v[i].id;
-    memcpy(poses[i].R, v[i].pose_R, sizeof(poses[i].R));
-    memcpy(poses[i].t, v[i].pose_t, sizeof(poses[i].t));
-    poses[i].err = v[i].pose_err[0] <= v[i].pose_err[1] ? v[i].pose_err[0] : v[i].pose_err[1];  // estimate_tag_pose
+    const DevDetection& v = cand[idx[i]];
+    poses[i].id = v.id;
+    memcpy(poses[i].R, v.pose_R, sizeof(poses[i].R));
+    memcpy(poses[i].t, v.pose_t, sizeof(poses[i].t));
+    poses[i].err = v.pose_err[0] <= v.pose_err[1] ? v.pose_err[0] : v.pose_err[1];  // estimate_tag_pose
   }
   for (int i = 0; i < n && i < cap; i++) {
+    const DevDetection& v = cand[idx[i]];
     at_detection& o = out[i];
-    o.id = v[i].id;
-    o.hamming = v[i].hamming;
-    o.decision_margin = v[i].decision_margin;
-    memcpy(o.H, v[i].H, sizeof(o.H));
-    memcpy(o.c, v[i].c, sizeof(o.c));
-    memcpy(o.p, v[i].p, sizeof(o.p));
+    o.id = v.id;
+    o.hamming = v.hamming;
+    o.decision_margin = v.decision_margin;
+    memcpy(o.H, v.H, sizeof(o.H));
+    memcpy(o.c, v.c, sizeof(o.c));
+    memcpy(o.p, v.p, sizeof(o.p));
   }
   return n;
 }
@@ -706,7 +717,7 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   if (!d || !out || cap < 1) return AT_E_INVALID;
   if (d->pending) return AT_E_INVALID;
   const int B = d->B;
-  uint64_t v[8] = {0};
+  uint64_t v[9] = {0};
   v[0] = (uint64_t)d->last_nframes;
   for (int f = 0; f < d->last_nframes; f++) {
     v[1] += d->h_ctrl[kCtlNpts * B + f];
@@ -717,9 +728,8 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   v[3] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts];
   v[4] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts + 1];
   v[7] = (uint64_t)d->host_wait_us;
-  uint64_t tail = (uint64_t)d->host_tail_us;
+  v[8] = (uint64_t)d->host_tail_us;
   const int n = std::min(cap, 9);
-  if (n > 8) out[8] = tail;
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
 }
@@ -844,9 +854,9 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       // the tiles' regions concatenated in tile order
       const size_t ntb = (size_t)g.ntb;
       std::vector<uint32_t> tc(ntb);
-      std::vector<uint64_t> all(ntb * kBndPts);
+      std::vector<uint64_t> all(ntb * (size_t)g.bnd_region);
       if (hipMemcpy(tc.data(), d->d.tcnt + frame * ntb, ntb * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-          hipMemcpy(all.data(), d->d.pts + frame * ntb * kBndPts, all.size() * 8, hipMemcpyDeviceToHost) !=
+          hipMemcpy(all.data(), d->d.pts + frame * ntb * g.bnd_region, all.size() * 8, hipMemcpyDeviceToHost) !=
               hipSuccess)
         return AT_E_HIP;
       size_t np = 0;
@@ -854,7 +864,7 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       if (bytes < np * 8) return AT_E_INVALID;
       size_t o = 0;
       for (size_t t = 0; t < ntb; t++) {
-        memcpy((uint8_t*)dst + o * 8, all.data() + t * kBndPts, tc[t] * 8);
+        memcpy((uint8_t*)dst + o * 8, all.data() + t * g.bnd_region, tc[t] * 8);
         o += tc[t];
       }
       return (long long)(np * 8);

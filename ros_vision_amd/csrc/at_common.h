@@ -35,7 +35,7 @@ constexpr int kPairEntCap = 65536;     // per-frame overflow (tile, pair, count)
 // each tile owns a fixed region of kBndPts points and kLdsPairSlots pair entries
 constexpr int kBndRows = 4;
 constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel (global region per tile)
-constexpr int kBndStage = 1536;                 // of which staged in LDS (1.5 per pixel)
+constexpr int kBndStage = 1024;                 // of which staged in LDS (1 per pixel; typical tiles hold ~0.7)
 constexpr int kLdsPairSlots = 512;
 constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
@@ -86,6 +86,7 @@ struct Geom {
   int BW, BH;           // 2x2 CCL blocks
   int CTX, CTY;         // CCL tiles
   int ctw;              // CCL tile width (32: latency mode, 64: throughput mode)
+  int bnd_region;       // points per k_boundary tile region (kBndPts)
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)
   int BTX, BTY, ntb;    // k_boundary tiles (64 x 4*kBndRows interior pixels each)
   uint32_t min_cluster; // max(24, min_cluster_pixels)

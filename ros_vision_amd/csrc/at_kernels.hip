@@ -775,7 +775,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   const int x = 1 + blockIdx.x * 64 + threadIdx.x;
   const uint32_t lane = lane_id();
   const size_t tb = (size_t)f * g.ntb + blockIdx.y * gridDim.x + blockIdx.x;
-  uint64_t* pts_out = b.pts + tb * kBndPts;
+  uint64_t* pts_out = b.pts + tb * g.bnd_region;
   for (int r = 0; r < kBndRows; r++) {
     const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
     const int y = ty0 + ly;
@@ -819,7 +819,8 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
     for (int dir = 0; dir < 4; dir++)
       if (pk[dir]) {
         if (pos < (uint32_t)kBndStage) s_pts[pos] = pk[dir];
-        else pts_out[pos] = pk[dir];
+        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = pk[dir];
+        else atomicOr(b.status + f, kStatusPointsOverflow);
         pos++;
       }
   }
@@ -842,7 +843,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   }
   __syncthreads();
   if (tid == 0) {
-    b.tcnt[tb] = total;
+    b.tcnt[tb] = min(total, (uint32_t)g.bnd_region);
     b.tent[tb] = s_nent;
   }
 }
@@ -1091,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
   }
   __syncthreads();
-  const uint64_t* pts = b.pts + tb * kBndPts;
+  const uint64_t* pts = b.pts + tb * g.bnd_region;
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
   for (uint32_t i = tid; i < n; i += 256) {
     const uint64_t key = pts[i];
