@@ -268,6 +268,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
   d->nblobwg = std::max(64, ncu * 2);
+  if (getenv("AT_BLOB_WG")) d->nblobwg = std::max(16, atoi(getenv("AT_BLOB_WG")));  // experiment: persistent grid size
 
   const size_t B = (size_t)d->B;
   const size_t npix = (size_t)W * H, nd = (size_t)g.Wd * g.Hd, nt = (size_t)g.TW * g.TH * 2;
