@@ -1061,34 +1061,45 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 // points' range of the pair segment with one atomic, then the tile's points
 // take consecutive slots of their entry (LDS cursor).  Pairs missing from the
 // tile's entries (LDS table overflow in k_boundary) reserve per point.
+constexpr int kGrpEnt = 128;  // tile entries with an LDS cursor (typical tiles: ~10)
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const int f = blockIdx.y;
   if (b.status[f] & (kStatusPairsOverflow | kStatusHashFull)) return;
-  __shared__ uint64_t s_hk[2 * kLdsPairSlots];
-  __shared__ uint32_t s_he[2 * kLdsPairSlots];
-  __shared__ uint32_t s_base[kLdsPairSlots], s_cur[kLdsPairSlots];
+  // the tile's first kGrpEnt pair entries: an LDS table (<= 50 % full) mapping the
+  // pair key to the entry, whose points take consecutive slots of the range the
+  // entry reserved with one atomic; the points of later entries (crowded tiles)
+  // reserve one slot each.  Points of pairs outside SelectBlobs' count bounds
+  // (P4's size filter) are dropped: nothing reads their segments.
+  __shared__ uint64_t s_hk[2 * kGrpEnt];
+  __shared__ uint32_t s_he[2 * kGrpEnt];
+  __shared__ uint32_t s_base[kGrpEnt], s_cur[kGrpEnt];
   const int tid = threadIdx.x;
   const size_t tb = (size_t)f * g.ntb + blockIdx.x;
   const uint32_t n = b.tcnt[tb], ne = b.tent[tb];
   const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
   const uint32_t* ht_off = b.ht_off + (size_t)f * kHashSlots;
+  const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
   uint32_t* ht_cur = b.ht_cur + (size_t)f * kHashSlots;
-  for (int i = tid; i < 2 * kLdsPairSlots; i += 256) s_hk[i] = 0;
+  constexpr uint32_t kDrop = 0xfffffffeu;
+  auto in_bounds = [&](uint32_t c) { return c >= g.min_cluster && c <= g.max_cluster; };
+  for (int i = tid; i < 2 * kGrpEnt; i += 256) s_hk[i] = 0;
   __syncthreads();
-  for (uint32_t e = tid; e < ne; e += 256) {
+  for (uint32_t e = tid; e < ne && e < (uint32_t)kGrpEnt; e += 256) {
     const uint64_t key = b.pent_key[tb * kLdsPairSlots + e];
     const uint32_t cnt = b.pent_cnt[tb * kLdsPairSlots + e];
     const uint32_t slot = ht_slot_find(ht_key, key);
-    s_base[e] = slot == 0xffffffffu ? 0u : ht_off[slot] + atomicAdd(ht_cur + slot, cnt);
+    uint32_t base = 0;
+    if (slot != 0xffffffffu) base = in_bounds(ht_cnt[slot]) ? ht_off[slot] + atomicAdd(ht_cur + slot, cnt) : kDrop;
+    s_base[e] = base;
     s_cur[e] = 0;
-    uint32_t h = (uint32_t)(mix_hash(key) & (2 * kLdsPairSlots - 1));
+    uint32_t h = (uint32_t)(mix_hash(key) & (2 * kGrpEnt - 1));
     while (true) {  // keys are distinct and the table is at most half full
       const uint64_t prev = atomicCAS((unsigned long long*)&s_hk[h], 0ull, (unsigned long long)key);
       if (prev == 0) {
         s_he[h] = e;
         break;
       }
-      h = (h + 1) & (2 * kLdsPairSlots - 1);
+      h = (h + 1) & (2 * kGrpEnt - 1);
     }
   }
   __syncthreads();
@@ -1097,22 +1108,22 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   for (uint32_t i = tid; i < n; i += 256) {
     const uint64_t key = pts[i];
     const uint64_t r01 = key >> 24;
-    uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kLdsPairSlots - 1));
+    uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
     uint32_t e = 0xffffffffu;
-    for (int probe = 0; probe < 2 * kLdsPairSlots; probe++) {
+    for (int probe = 0; probe < 2 * kGrpEnt; probe++) {
       const uint64_t k = s_hk[h];
       if (k == r01) { e = s_he[h]; break; }
       if (k == 0) break;
-      h = (h + 1) & (2 * kLdsPairSlots - 1);
+      h = (h + 1) & (2 * kGrpEnt - 1);
     }
-    uint32_t pos;
     if (e != 0xffffffffu) {
-      pos = s_base[e] + atomicAdd(&s_cur[e], 1u);
+      if (s_base[e] == kDrop) continue;
+      grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = key;
     } else {
       const uint32_t slot = ht_slot_find(ht_key, r01);
-      pos = ht_off[slot] + atomicAdd(ht_cur + slot, 1u);
+      if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) continue;
+      grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = key;
     }
-    grp[pos] = key;
   }
 }
 

@@ -9,7 +9,7 @@
 # Output: gpurun_out/$TAG/...   usage: bash tools/profile_round.sh TAG [BATCH]
 set -euo pipefail
 TAG=${1:-prof}
-BATCH=${2:-32}
+BATCH=${2:-128}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -33,6 +33,10 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/cali
   $ROOT/tools/pmc_calib > "$OUT/calib_bytes.csv" 2> "$OUT/calib_fetch.err"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib_write" -o run -- \
   $ROOT/tools/pmc_calib > /dev/null 2> "$OUT/calib_write.err"
+python3 $ROOT/tools/pmc_calib.py "$OUT" > /dev/null
 cd "$ROOT"
+python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" "$OUT/pmc_write/run_counter_collection.csv" $BATCH 1280 720 "$OUT/pmc_traffic.json" > /dev/null
+cp "$OUT/pmc_traffic.json" profiles/pmc_traffic.json  # the bench line below reads it
+python3 tools/pmc_agg.py "$OUT/pmc_sq_a/run_counter_collection.csv" "$OUT/pmc_sq_b/run_counter_collection.csv" > "$OUT/sq_counters_agg.txt"
 timeout -k 10 400 python3 bench.py --batch $BATCH > "$OUT/bench.json" 2> "$OUT/bench.err"
 find "$OUT" -name "*.csv" | sort
