@@ -19,7 +19,7 @@ class Params(C.Structure):
         ("k1", C.c_double), ("k2", C.c_double), ("p1", C.c_double), ("p2", C.c_double), ("k3", C.c_double),
         ("min_white_black_diff", C.c_int), ("min_cluster_pixels", C.c_int), ("max_nmaxima", C.c_int),
         ("max_line_fit_mse", C.c_float), ("cos_critical_rad", C.c_double),
-        ("decode_sharpening", C.c_double), ("refine_edges", C.c_int),
+        ("decode_sharpening", C.c_double), ("refine_edges", C.c_int), ("family", C.c_char_p),
     ]
 
 
@@ -68,11 +68,16 @@ def lib():
             getattr(L, name).restype = C.c_int
             getattr(L, name).argtypes = [C.c_void_p]
         L.ao_family_code.restype = C.c_uint64
-        L.ao_family_code.argtypes = [C.c_int]
+        L.ao_family_code.argtypes = [C.c_char_p, C.c_int]
         L.ao_family_ncodes.restype = C.c_int
+        L.ao_family_ncodes.argtypes = [C.c_char_p]
+        L.ao_family_nbits.restype = C.c_int
+        L.ao_family_nbits.argtypes = [C.c_char_p]
         L.ao_family_id.restype = C.c_int
-        L.ao_family_id.argtypes = [C.c_int]
-        L.ao_family_bit.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.ao_family_id.argtypes = [C.c_char_p, C.c_int]
+        L.ao_family_bit.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.ao_rotate90_n.restype = C.c_uint64
+        L.ao_rotate90_n.argtypes = [C.c_uint64, C.c_int]
         for n in ["ao_det_atan2f", "ao_det_hypotf"]:
             getattr(L, n).restype = C.c_float
             getattr(L, n).argtypes = [C.c_float, C.c_float]
@@ -95,21 +100,25 @@ def build():
     subprocess.run(["make", "-C", _HERE, "-s"], check=True)
 
 
-def default_params(width, height):
+FAMILIES = ("tag36h11", "tag25h9", "tag16h5")
+
+
+def default_params(width, height, family="tag36h11"):
     p = Params()
     lib().ao_default_params(C.byref(p), width, height)
+    p.family = family.encode()
     return p
 
 
 class Oracle:
     """One oracle detector instance (mirrors GpuDetector's lifetime)."""
 
-    def __init__(self, width, height, params=None):
+    def __init__(self, width, height, params=None, family="tag36h11"):
         self.W, self.H = width, height
-        self.params = params if params is not None else default_params(width, height)
+        self.params = params if params is not None else default_params(width, height, family)
         self.h = lib().ao_create(C.byref(self.params))
         if not self.h:
-            raise ValueError("oracle: unsupported frame size %dx%d" % (width, height))
+            raise ValueError("oracle: unsupported frame size %dx%d or family" % (width, height))
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -206,6 +215,23 @@ def set_fp_perturb(mask: int):
     lib().ao_set_fp_perturb(int(mask))
 
 
-def family_entries():
+def family_entries(family="tag36h11"):
     L = lib()
-    return [(int(L.ao_family_id(i)), int(L.ao_family_code(i))) for i in range(L.ao_family_ncodes())]
+    f = family.encode()
+    n = L.ao_family_ncodes(f)
+    if n < 0:
+        raise ValueError("oracle: unknown family %r" % family)
+    return [(int(L.ao_family_id(f, i)), int(L.ao_family_code(f, i))) for i in range(n)]
+
+
+def family_layout(family="tag36h11"):
+    """(bit_x, bit_y) lists of the family's 3.x layout."""
+    L = lib()
+    f = family.encode()
+    xs, ys = [], []
+    for i in range(L.ao_family_nbits(f)):
+        x, y = C.c_int(), C.c_int()
+        L.ao_family_bit(f, i, C.byref(x), C.byref(y))
+        xs.append(x.value)
+        ys.append(y.value)
+    return xs, ys

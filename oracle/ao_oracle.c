@@ -129,31 +129,96 @@ float ao_det_hypotf(float a, float b) {
 #define det_hypotf ao_det_hypotf
 
 /* ------------------------------------------------------------------------- */
-/* tag36h11 family (third party: apriltag 3.x tag36h11.c)                      */
+/* tag families (third party: apriltag 3.x tag36h11.c, tag25h9.c, tag16h5.c;    */
+/* selected by name in setup_tag_family, apriltag_utils.cu:10-32)              */
 /* ------------------------------------------------------------------------- */
 typedef struct { int id; uint64_t code; } CodeEntry;
-static const CodeEntry kCodes[] = {
+static const CodeEntry kCodes36h11[] = {
 #include "ao_tag36h11_codes.inc"
 };
-static const int kNumCodes = (int)(sizeof(kCodes) / sizeof(kCodes[0]));
-/* bit_x / bit_y of tag36h11 (apriltag 3.x spiral layout; width_at_border 8) */
-static const int kBitX[36] = {1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4,
-                              6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3};
-static const int kBitY[36] = {1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3,
-                              6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4};
-enum { kWidthAtBorder = 8, kTotalWidth = 10, kNBits = 36, kReversedBorder = 0, kMaxHamming = 2 };
+static const CodeEntry kCodes25h9[] = {
+#include "ao_tag25h9_codes.inc"
+};
+static const CodeEntry kCodes16h5[] = {
+#include "ao_tag16h5_codes.inc"
+};
+/* the classic square families: d x d data cells inside a one-cell black border
+ * (width_at_border = d + 2), one white cell outside it (total_width = d + 4),
+ * normal border; bits in the 3.x spiral order (bit_x/bit_y of tagXXhY.c) */
+typedef struct {
+  const char *name;
+  int d, nbits, width_at_border, total_width, reversed_border;
+  const CodeEntry *codes;
+  int ncodes;
+  int bitx[64], bity[64];
+} Family;
+#define AO_NCODES(a) ((int)(sizeof(a) / sizeof((a)[0])))
+static Family kFamilies[] = {
+    {"tag36h11", 6, 36, 8, 10, 0, kCodes36h11, AO_NCODES(kCodes36h11), {0}, {0}},
+    {"tag25h9", 5, 25, 7, 9, 0, kCodes25h9, AO_NCODES(kCodes25h9), {0}, {0}},
+    {"tag16h5", 4, 16, 6, 8, 0, kCodes16h5, AO_NCODES(kCodes16h5), {0}, {0}},
+};
+enum { kNumFamilies = 3, kMaxHamming = 2 }; /* apriltag_detector_add_family: 2 bits corrected */
 
-int ao_family_ncodes(void) { return kNumCodes; }
-uint64_t ao_family_code(int i) { return (i >= 0 && i < kNumCodes) ? kCodes[i].code : 0; }
-int ao_family_id(int i) { return (i >= 0 && i < kNumCodes) ? kCodes[i].id : -1; }
-void ao_family_bit(int i, int *x, int *y) { *x = kBitX[i]; *y = kBitY[i]; }
-
-/* apriltag.c rotate90 for nbits = 36 (numBits % 4 == 0) */
-uint64_t ao_rotate90(uint64_t w) {
-  const int p = 36;
-  w = ((w >> 0) << (p / 4)) | (w >> (3 * p / 4));
-  return w & ((1ULL << 36) - 1);
+/* 3.x layout of tagXXhY.c: the upper triangle of the top-left quadrant row by
+ * row (y = 1 .. d/2, x = y .. d-y), that block rotated by 90 degrees three more
+ * times ((x, y) -> (d+1-y, x)), the centre cell last when d is odd */
+static void family_layout(Family *f) {
+  int n = 0;
+  for (int r = 0; r < 4; r++)
+    for (int y = 1; y <= f->d / 2; y++)
+      for (int x = y; x <= f->d - y; x++) {
+        int xx = x, yy = y;
+        for (int i = 0; i < r; i++) { const int t = xx; xx = f->d + 1 - yy; yy = t; }
+        f->bitx[n] = xx; f->bity[n] = yy; n++;
+      }
+  if (f->d & 1) { f->bitx[n] = f->d / 2 + 1; f->bity[n] = f->d / 2 + 1; n++; }
 }
+
+static const Family *family_by_name(const char *name) {
+  static int init = 0;
+  if (!init) {
+    for (int i = 0; i < kNumFamilies; i++) family_layout(&kFamilies[i]);
+    init = 1;
+  }
+  if (!name) name = "tag36h11";
+  for (int i = 0; i < kNumFamilies; i++)
+    if (!strcmp(kFamilies[i].name, name)) return &kFamilies[i];
+  return NULL;
+}
+
+int ao_family_ncodes(const char *fam) {
+  const Family *f = family_by_name(fam);
+  return f ? f->ncodes : -1;
+}
+uint64_t ao_family_code(const char *fam, int i) {
+  const Family *f = family_by_name(fam);
+  return (f && i >= 0 && i < f->ncodes) ? f->codes[i].code : 0;
+}
+int ao_family_id(const char *fam, int i) {
+  const Family *f = family_by_name(fam);
+  return (f && i >= 0 && i < f->ncodes) ? f->codes[i].id : -1;
+}
+void ao_family_bit(const char *fam, int i, int *x, int *y) {
+  const Family *f = family_by_name(fam);
+  *x = f ? f->bitx[i] : -1;
+  *y = f ? f->bity[i] : -1;
+}
+int ao_family_nbits(const char *fam) {
+  const Family *f = family_by_name(fam);
+  return f ? f->nbits : -1;
+}
+
+/* apriltag.c rotate90 (3.x): the spiral layout turns a 90-degree rotation into
+ * a rotation of the bit string by nbits/4, the centre bit (LSB) fixed for odd d */
+uint64_t ao_rotate90_n(uint64_t w, int nbits) {
+  int p = nbits;
+  uint64_t l = 0;
+  if (nbits % 4 == 1) { p = nbits - 1; l = 1; }
+  w = ((w >> l) << (p / 4 + l)) | (w >> (3 * p / 4 + l) << l) | (w & l);
+  return w & ((1ULL << nbits) - 1);
+}
+uint64_t ao_rotate90(uint64_t w) { return ao_rotate90_n(w, 36); }
 
 /* ------------------------------------------------------------------------- */
 /* state                                                                      */
@@ -179,6 +244,7 @@ typedef struct {
 
 struct ao_state {
   ao_params p;
+  const Family *fam;
   int W, H, Wd, Hd;
   int min_tag_width;
   int status;
@@ -227,11 +293,14 @@ void ao_default_params(ao_params *p, int width, int height) {
 ao_state *ao_create(const ao_params *p) {
   if (p->width % 8 || p->height % 8) return NULL;
   if ((long)p->width * p->height >= (1L << 22)) return NULL; /* apriltag_gpu.cu:774 */
+  const Family *fam = family_by_name(p->family);
+  if (!fam) return NULL; /* setup_tag_family: unknown name (apriltag_utils.cu:26-29) */
   ao_state *s = (ao_state *)calloc(1, sizeof(ao_state));
   s->p = *p;
+  s->fam = fam;
   s->W = p->width; s->H = p->height; s->Wd = s->W / 2; s->Hd = s->H / 2;
-  /* GpuDetector ctor, apriltag_gpu.cu:169-181: width_at_border 8 / quad_decimate 2 */
-  s->min_tag_width = kWidthAtBorder / 2;
+  /* GpuDetector ctor, apriltag_gpu.cu:169-181: width_at_border / quad_decimate 2 */
+  s->min_tag_width = fam->width_at_border / 2;
   if (s->min_tag_width < 3) s->min_tag_width = 3;
   size_t npix = (size_t)s->W * s->H, nd = (size_t)s->Wd * s->Hd;
   size_t nt = (size_t)(s->Wd / 4) * (s->Hd / 4);
@@ -517,7 +586,7 @@ static float ext_dot(const Extents *e) {
   return (float)(a - b + c);
 }
 
-/* SelectBlobs (apriltag_gpu.cu:522-575) for tag36h11: normal border only */
+/* SelectBlobs (apriltag_gpu.cu:522-575) for one family (normal_border_/reversed_border_ from it) */
 static int select_blob(const ao_state *s, const Extents *e) {
   const uint32_t minc = s->p.min_cluster_pixels > 24 ? (uint32_t)s->p.min_cluster_pixels : 24u;
   const uint32_t maxc = (uint32_t)(2 * (s->W + s->H)); /* :871 */
@@ -525,7 +594,7 @@ static int select_blob(const ao_state *s, const Extents *e) {
   if (e->count > maxc) return 0;
   if ((e->max_x - e->min_x) * (e->max_y - e->min_y) < s->min_tag_width) return 0;
   const int quad_reversed = (double)ext_dot(e) < 0.0;
-  const int reversed_border = kReversedBorder, normal_border = !kReversedBorder;
+  const int reversed_border = s->fam->reversed_border, normal_border = !s->fam->reversed_border;
   if (!reversed_border && quad_reversed) return 0;
   if (!normal_border && !quad_reversed) return 0;
   return 1;
@@ -841,7 +910,7 @@ static void stage_quads(ao_state *s) {
     if (!f->valid) continue;
     ao_quad qc;
     qc.blob_index = f->blob_index;
-    qc.reversed_border = kReversedBorder;
+    qc.reversed_border = s->fam->reversed_border;
     double lines[4][4];
     for (int k = 0; k < 4; k++) host_fit_line(f, k, lines[k], lines[k] + 2);
     int bad = 0;
@@ -1082,7 +1151,9 @@ static double value_for_pixel(const ao_state *s, double px, double py) {
 
 static float quad_decode(const ao_state *s, const double H[9], int *out_id, int *out_ham, int *out_rot,
                          uint64_t *out_rcode) {
-  const float wab = (float)kWidthAtBorder;
+  const Family *fam = s->fam;
+  const int wabi = fam->width_at_border, tw = fam->total_width;
+  const float wab = (float)wabi;
   const float patterns[40] = {
       -0.5f, 0.5f, 0, 1, 1,   0.5f, 0.5f, 0, 1, 0,   wab + 0.5f, .5f, 0, 1, 1,  wab - 0.5f, .5f, 0, 1, 0,
       0.5f, -0.5f, 1, 0, 1,   0.5f, 0.5f, 1, 0, 0,   0.5f, wab + 0.5f, 1, 0, 1, 0.5f, wab - 0.5f, 1, 0, 0};
@@ -1091,9 +1162,9 @@ static float quad_decode(const ao_state *s, const double H[9], int *out_id, int 
   for (int pi = 0; pi < 8; pi++) {
     const float *pat = &patterns[pi * 5];
     const int is_white = (int)pat[4];
-    for (int i = 0; i < kWidthAtBorder; i++) {
-      const double tagx01 = (double)((pat[0] + (float)i * pat[2]) / (float)kWidthAtBorder);
-      const double tagy01 = (double)((pat[1] + (float)i * pat[3]) / (float)kWidthAtBorder);
+    for (int i = 0; i < wabi; i++) {
+      const double tagx01 = (double)((pat[0] + (float)i * pat[2]) / (float)wabi);
+      const double tagy01 = (double)((pat[1] + (float)i * pat[3]) / (float)wabi);
       const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
       double px, py;
       hproject(H, tagx, tagy, &px, &py);
@@ -1106,27 +1177,27 @@ static float quad_decode(const ao_state *s, const double H[9], int *out_id, int 
   }
   gm_solve(&wm);
   gm_solve(&bm);
-  if ((gm_interp(&wm, 0, 0) - gm_interp(&bm, 0, 0) < 0) != kReversedBorder) return -1;
+  if ((gm_interp(&wm, 0, 0) - gm_interp(&bm, 0, 0) < 0) != fam->reversed_border) return -1;
   float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
-  double values[kTotalWidth * kTotalWidth];
+  double values[16 * 16];
   memset(values, 0, sizeof(values));
-  const int min_coord = (kWidthAtBorder - kTotalWidth) / 2;
-  for (int i = 0; i < kNBits; i++) {
-    const int bity = kBitY[i], bitx = kBitX[i];
-    const double tagx01 = (bitx + 0.5) / kWidthAtBorder, tagy01 = (bity + 0.5) / kWidthAtBorder;
+  const int min_coord = (wabi - tw) / 2;
+  for (int i = 0; i < fam->nbits; i++) {
+    const int bity = fam->bity[i], bitx = fam->bitx[i];
+    const double tagx01 = (bitx + 0.5) / wabi, tagy01 = (bity + 0.5) / wabi;
     const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
     double px, py;
     hproject(H, tagx, tagy, &px, &py);
     const double v = value_for_pixel(s, px, py);
     if (v == -1) continue;
     const double thresh = (gm_interp(&bm, tagx, tagy) + gm_interp(&wm, tagx, tagy)) / 2.0;
-    values[kTotalWidth * (bity - min_coord) + bitx - min_coord] = v - thresh;
+    values[tw * (bity - min_coord) + bitx - min_coord] = v - thresh;
   }
-  /* sharpen (apriltag.c) */
+  /* sharpen (apriltag.c) over the total_width x total_width grid */
   {
-    double sh[kTotalWidth * kTotalWidth];
+    double sh[16 * 16];
     static const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
-    const int size = kTotalWidth;
+    const int size = tw;
     for (int y = 0; y < size; y++)
       for (int x = 0; x < size; x++) {
         sh[y * size + x] = 0;
@@ -1141,24 +1212,25 @@ static float quad_decode(const ao_state *s, const double H[9], int *out_id, int 
         values[y * size + x] = values[y * size + x] + s->p.decode_sharpening * sh[y * size + x];
   }
   uint64_t rcode = 0;
-  for (int i = 0; i < kNBits; i++) {
-    const int bity = kBitY[i], bitx = kBitX[i];
+  for (int i = 0; i < fam->nbits; i++) {
+    const int bity = fam->bity[i], bitx = fam->bitx[i];
     rcode = rcode << 1;
-    const double v = values[kTotalWidth * (bity - min_coord) + bitx - min_coord];
+    const double v = values[tw * (bity - min_coord) + bitx - min_coord];
     if (v > 0) { white_score = (float)(white_score + v); white_cnt++; rcode |= 1; }
     else { black_score = (float)(black_score - v); black_cnt++; }
   }
   *out_rcode = rcode;
-  /* quick_decode_codeword: first rotation with a codeword within kMaxHamming */
+  /* quick_decode_codeword: first rotation with a codeword within kMaxHamming
+   * (the family's codes are >= 5 apart, so at most one entry matches a rotation) */
   *out_id = 65535; *out_ham = 255; *out_rot = 0;
   for (int r = 0; r < 4; r++) {
     int found = 0;
-    for (int c = 0; c < kNumCodes; c++) {
-      const int hd = __builtin_popcountll(rcode ^ kCodes[c].code);
-      if (hd <= kMaxHamming) { *out_id = kCodes[c].id; *out_ham = hd; *out_rot = r; found = 1; break; }
+    for (int c = 0; c < fam->ncodes; c++) {
+      const int hd = __builtin_popcountll(rcode ^ fam->codes[c].code);
+      if (hd <= kMaxHamming) { *out_id = fam->codes[c].id; *out_ham = hd; *out_rot = r; found = 1; break; }
     }
     if (found) break;
-    rcode = ao_rotate90(rcode);
+    rcode = ao_rotate90_n(rcode, fam->nbits);
   }
   return (float)fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
 }

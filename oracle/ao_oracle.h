@@ -38,6 +38,7 @@ typedef struct {
   double cos_critical_rad;         /* qtp.cos_critical_rad = cos(10 deg) */
   double decode_sharpening;        /* td->decode_sharpening = 0.25 */
   int refine_edges;                /* td->refine_edges = 1 */
+  const char *family;              /* "tag36h11" (default when NULL), "tag25h9", "tag16h5" */
 } ao_params;
 
 typedef struct {
@@ -98,11 +99,12 @@ int ao_status(const ao_state *s);                  /* 0 ok, <0 capacity error */
 uint64_t ao_quad_rcode(const ao_state *s, int i);   /* sampled code word of quad i */
 float ao_quad_margin(const ao_state *s, int i);
 
-/* tag36h11 family */
-int ao_family_ncodes(void);
-uint64_t ao_family_code(int i);   /* i-th known entry */
-int ao_family_id(int i);          /* its tag id */
-void ao_family_bit(int i, int *x, int *y);
+/* tag families by name (NULL = tag36h11); -1 / 0 for an unknown name */
+int ao_family_ncodes(const char *fam);
+uint64_t ao_family_code(const char *fam, int i);   /* i-th entry */
+int ao_family_id(const char *fam, int i);          /* its tag id */
+void ao_family_bit(const char *fam, int i, int *x, int *y);
+int ao_family_nbits(const char *fam);
 
 /* deterministic math (exported for the accuracy tests) */
 float ao_det_atan2f(float y, float x);
@@ -118,7 +120,8 @@ int ao_estimate_tag_pose(const double H[9], const double corners[4][2], double f
                          double tagsize, double R[9], double t[3], double err[2]);
 
 /* helpers exposed for tests */
-uint64_t ao_rotate90(uint64_t w);
+uint64_t ao_rotate90(uint64_t w);                 /* 36 bits */
+uint64_t ao_rotate90_n(uint64_t w, int nbits);
 int ao_unrank(int i, int *m0, int *m1, int *m2, int *m3);
 /* ulp-sensitivity hook (tests only): see ao_oracle.c */
 void ao_set_fp_perturb(int mask);

@@ -21,7 +21,6 @@
 #include "at_common.h"
 
 namespace at {
-hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n);
 hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint32_t* size, uint32_t* out, int Wd,
                             int Hd, hipStream_t st);
 hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd, hipStream_t st);
@@ -36,7 +35,73 @@ struct CodeEntry {
 static const CodeEntry kTag36h11[] = {
 #include "at_tag36h11_codes.inc"
 };
-static const int kTag36h11Known = (int)(sizeof(kTag36h11) / sizeof(kTag36h11[0]));
+static const CodeEntry kTag25h9[] = {
+#include "at_tag25h9_codes.inc"
+};
+static const CodeEntry kTag16h5[] = {
+#include "at_tag16h5_codes.inc"
+};
+
+// The families setup_tag_family selects by name (apriltag_utils.cu:10-32).  The
+// classic square ones are built: d x d data cells, a one-cell black border
+// (width_at_border d + 2), a white quiet zone (total_width d + 4), normal border,
+// 2 bits corrected (apriltag_detector_add_family).  The apriltag 3 layouts
+// (tagCircle21h7, tagCircle49h12, tagStandard41h12, tagStandard52h13,
+// tagCustom48h12) are named but have no codebook here: their tables live in the
+// un-vendored upstream sources and could not be regenerated offline, so
+// at_create reports AT_E_FAMILY for them.
+struct FamilyInfo {
+  const char* name;
+  int d;
+  const CodeEntry* codes;
+  int ncodes;
+};
+#define AT_NCODES(a) ((int)(sizeof(a) / sizeof((a)[0])))
+static const FamilyInfo kFamilies[] = {
+    {"tag36h11", 6, kTag36h11, AT_NCODES(kTag36h11)},
+    {"tag25h9", 5, kTag25h9, AT_NCODES(kTag25h9)},
+    {"tag16h5", 4, kTag16h5, AT_NCODES(kTag16h5)},
+};
+
+static const FamilyInfo* find_family(const char* name) {
+  if (!name) return nullptr;
+  for (const FamilyInfo& f : kFamilies)
+    if (!strcmp(f.name, name)) return &f;
+  return nullptr;
+}
+
+// apriltag_family_t fields quad_decode_index reads; bit_x / bit_y in the 3.x
+// layout of tagXXhY.c: the upper triangle of the top-left quadrant row by row,
+// rotated by 90 degrees three more times ((x, y) -> (d+1-y, x)), the centre
+// cell last when d is odd
+static FamilyDesc family_desc(const FamilyInfo& f) {
+  FamilyDesc fd{};
+  const int d = f.d;
+  fd.nbits = d * d;
+  fd.width_at_border = d + 2;
+  fd.total_width = d + 4;
+  fd.reversed_border = 0;
+  fd.ncodes = f.ncodes;
+  int n = 0;
+  for (int r = 0; r < 4; r++)
+    for (int y = 1; y <= d / 2; y++)
+      for (int x = y; x <= d - y; x++) {
+        int xx = x, yy = y;
+        for (int i = 0; i < r; i++) {
+          const int t = xx;
+          xx = d + 1 - yy;
+          yy = t;
+        }
+        fd.bitx[n] = (int8_t)xx;
+        fd.bity[n] = (int8_t)yy;
+        n++;
+      }
+  if (d & 1) {
+    fd.bitx[n] = (int8_t)(d / 2 + 1);
+    fd.bity[n] = (int8_t)(d / 2 + 1);
+  }
+  return fd;
+}
 }  // namespace at
 
 using namespace at;
@@ -122,15 +187,16 @@ const char* at_strerror(int code) {
 }
 
 int at_family_num_known(const char* family) {
-  if (!family || strcmp(family, "tag36h11") != 0) return AT_E_FAMILY;
-  return kTag36h11Known;
+  const FamilyInfo* f = find_family(family);
+  return f ? f->ncodes : AT_E_FAMILY;
 }
 
 int at_family_entry(const char* family, int i, int* id, uint64_t* code) {
-  if (!family || strcmp(family, "tag36h11") != 0) return AT_E_FAMILY;
-  if (i < 0 || i >= kTag36h11Known) return AT_E_INVALID;
-  if (id) *id = kTag36h11[i].id;
-  if (code) *code = kTag36h11[i].code;
+  const FamilyInfo* f = find_family(family);
+  if (!f) return AT_E_FAMILY;
+  if (i < 0 || i >= f->ncodes) return AT_E_INVALID;
+  if (id) *id = f->codes[i].id;
+  if (code) *code = f->codes[i].code;
   return AT_OK;
 }
 
@@ -184,7 +250,8 @@ void at_destroy(at_detector* d) {
 int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (!cfg || !cam || !out) return AT_E_INVALID;
   *out = nullptr;
-  if (!cfg->family || strcmp(cfg->family, "tag36h11") != 0) return AT_E_FAMILY;
+  const FamilyInfo* fam = find_family(cfg->family);
+  if (!fam) return AT_E_FAMILY;
   const int W = cfg->width, H = cfg->height;
   // GpuDetector preconditions (apriltag_gpu.cu:166-167, 754-755, 774; line_fit_filter.cu:1205)
   if (W <= 16 || H <= 16 || W % 8 || H % 8 || (long)W * H >= (1L << 22)) return AT_E_INVALID;
@@ -195,7 +262,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) return AT_E_HIP;
   at_detector* d = new at_detector();  // value-initialised: every pointer null
   d->cfg = *cfg;
-  d->cfg.family = "tag36h11";
+  d->cfg.family = fam->name;
   d->cam = *cam;
   d->device = cfg->device;
   d->B = cfg->max_batch;
@@ -219,7 +286,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   }
   g.min_cluster = (uint32_t)std::max(24, cfg->min_cluster_pixels);
   g.max_cluster = (uint32_t)(2 * (W + H));
-  g.min_tag_width = std::max(3, 8 / 2);  // tag36h11 width_at_border 8 / quad_decimate 2
+  // GpuDetector ctor (apriltag_gpu.cu:169-181): width_at_border / quad_decimate, >= 3
+  g.min_tag_width = std::max(3, (fam->d + 2) / 2);
   Params& p = d->prm;
   p.min_white_black_diff = cfg->min_white_black_diff;
   p.max_line_fit_mse = cfg->max_line_fit_mse;
@@ -233,6 +301,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
   p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
   p.pipe_stop = getenv("AT_DIAG_PIPE_STOP") ? atoi(getenv("AT_DIAG_PIPE_STOP")) : 0;
+  p.fam = family_desc(*fam);
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {
     at_destroy(d);
@@ -353,13 +422,21 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.ctrl = d->d_ctrl;
   b.ctrl_words = (uint32_t)d->ctrl_words;
   {
-    std::vector<uint64_t> codes(kTag36h11Known);
-    std::vector<int> ids(kTag36h11Known);
-    for (int i = 0; i < kTag36h11Known; i++) {
-      codes[i] = kTag36h11[i].code;
-      ids[i] = kTag36h11[i].id;
+    // this detector's codebook in HBM (k_decode matches every entry in parallel)
+    std::vector<uint64_t> codes(fam->ncodes);
+    std::vector<int32_t> ids(fam->ncodes);
+    for (int i = 0; i < fam->ncodes; i++) {
+      codes[i] = fam->codes[i].code;
+      ids[i] = fam->codes[i].id;
     }
-    if (upload_codebook(codes.data(), ids.data(), kTag36h11Known) != hipSuccess) return fail(AT_E_HIP);
+    uint64_t* dc = (uint64_t*)dalloc(codes.size() * 8);
+    int32_t* di = (int32_t*)dalloc(ids.size() * 4);
+    if (oom) return fail(AT_E_NOMEM);
+    if (hipMemcpy(dc, codes.data(), codes.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(di, ids.data(), ids.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(AT_E_HIP);
+    b.book_code = dc;
+    b.book_id = di;
   }
   // size arrays are read for every label by k_boundary: start defined
   if (hipMemsetAsync(b.size, 0, B * nd * 4, d->st) != hipSuccess) return fail(AT_E_HIP);

@@ -78,6 +78,19 @@ constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config
 constexpr int kQuadCandPerFrame = kMaxPairs;  // accepted quads queued for decode, per frame
 constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections per frame (before reconcile)
 constexpr int kMaxCodes = 1024;               // codebook entries (tag36h11: 587)
+constexpr int kMaxFamilyBits = 64;
+
+// Tag family as quad_decode_index uses it (apriltag_family_t: nbits, bit_x/bit_y,
+// width_at_border, total_width, reversed_border); the codebook itself lives in
+// HBM (DevBufs::book_code / book_id), one per detector.
+struct FamilyDesc {
+  int nbits;            // data bits (16, 25, 36)
+  int width_at_border;  // cells across the black border (d + 2)
+  int total_width;      // cells across incl. the white quiet zone (d + 4)
+  int reversed_border;
+  int ncodes;
+  int8_t bitx[kMaxFamilyBits], bity[kMaxFamilyBits];  // 3.x layout, border coordinates
+};
 
 // Frame geometry (all derived from W, H).
 struct Geom {
@@ -107,6 +120,7 @@ struct Params {
   int taps;       // write the sorted IndexPoint parity tap (AT_STAGE_BLOB_POINTS) over the grouped points
   int wide_blob;  // AT_WIDE_BLOB=1: 512-thread large-blob teams at every batch size (experiment)
   int pipe_stop;  // diagnostics only (AT_DIAG_PIPE_STOP): launch the stages < N only; 0 = all
+  FamilyDesc fam;
 };
 constexpr int kProbeWords = 256;
 
@@ -206,6 +220,8 @@ struct DevBufs {
   QuadCand* qcand;    // [qcand_cap]
   uint32_t qcand_cap;
   double* rsamp;      // [decode workgroups][2][kMaxRefineSamples - kLdsRefine] refine samples past LDS
+  const uint64_t* book_code;  // [fam.ncodes] codebook (3.x bit order)
+  const int32_t* book_id;     // [fam.ncodes] tag id of each code
   // per-workgroup scratch of the blob kernel
   uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
                       // (pathological blobs only; every other per-blob array lives in LDS)

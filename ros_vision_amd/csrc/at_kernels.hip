@@ -141,18 +141,6 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 }
 
 
-struct DevCodebook {
-  int n;
-  uint64_t code[kMaxCodes];
-  int id[kMaxCodes];
-};
-__constant__ DevCodebook c_book;
-
-// tag36h11 bit layout (apriltag 3.x)
-__constant__ int c_bitx[36] = {1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4,
-                               6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3};
-__constant__ int c_bity[36] = {1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3,
-                               6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4};
 __constant__ float c_filter[7] = {0.01110899634659290314f, 0.13533528149127960205f, 0.60653066635131835938f,
                                   1.00000000000000000000f, 0.60653066635131835938f, 0.13533528149127960205f,
                                   0.01110899634659290314f};
@@ -1383,10 +1371,6 @@ __device__ void gm_solve(GrayModel& g) {
 }
 __device__ __forceinline__ double gm_interp(const GrayModel& g, double x, double y) {
   return g.C[0] * x + g.C[1] * y + g.C[2];
-}
-
-__device__ __forceinline__ uint64_t rotate90_36(uint64_t w) {
-  return ((w << 9) | (w >> 27)) & ((1ull << 36) - 1);
 }
 
 // lexicographic 4-combinations of 10 maxima == Unrank (line_fit_filter.cu:709-728)
@@ -2658,10 +2642,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // decision scores) run on one lane in the reference's order.
 // ---------------------------------------------------------------------------
 constexpr int kDecodeThreads = 64;
-// quad_decode border patterns (x0, y0, dx, dy, is_white) for width_at_border 8
-__constant__ float c_border_pat[8][5] = {{-0.5f, 0.5f, 0, 1, 1}, {0.5f, 0.5f, 0, 1, 0}, {8.5f, .5f, 0, 1, 1},
-                                         {7.5f, .5f, 0, 1, 0},   {0.5f, -0.5f, 1, 0, 1}, {0.5f, 0.5f, 1, 0, 0},
-                                         {0.5f, 8.5f, 1, 0, 1},  {0.5f, 7.5f, 1, 0, 0}};
+// quad_decode border patterns (x0, y0, dx, dy; white for even p): left white /
+// black column, right white / black column, top white / black row, bottom white /
+// black row, in float as upstream's `float patterns[]` (wab = width_at_border)
+__device__ __forceinline__ void border_pattern(int p, float wab, float& x0, float& y0, float& dx, float& dy) {
+  const float far_ = (p & 1) ? wab - 0.5f : wab + 0.5f;
+  const float near_ = (p & 1) ? 0.5f : -0.5f;
+  const int side = p >> 1;  // 0 left, 1 right, 2 top, 3 bottom
+  const float a = (side == 0 || side == 2) ? near_ : far_;
+  if (side < 2) { x0 = a; y0 = 0.5f; dx = 0; dy = 1; }
+  else { x0 = 0.5f; y0 = a; dx = 1; dy = 0; }
+}
+
+// apriltag.c rotate90 (3.x spiral layout): a rotation of the bit string by
+// nbits/4, the centre bit (LSB) fixed when nbits % 4 == 1
+__device__ __forceinline__ uint64_t rotate90_n(uint64_t w, int nbits) {
+  int p = nbits;
+  uint64_t l = 0;
+  if (nbits % 4 == 1) { p = nbits - 1; l = 1; }
+  w = ((w >> l) << (p / 4 + l)) | (w >> (3 * p / 4 + l) << l) | (w & l);
+  return w & ((1ull << nbits) - 1);
+}
+constexpr int kMaxTotalWidth = 12;  // total_width of the largest family layout (d <= 8)
 // cos / sin of rot * pi/2 as libm returns them (quad_decode's rotation of H)
 __constant__ double c_rot_c[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
 __constant__ double c_rot_s[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
@@ -2682,7 +2684,7 @@ struct DecodeShared {
   double gmx[64], gmy[64], gmv[64];
   int gmvalid[64];
   double wC[3], bC[3];
-  double values[100];
+  double values[kMaxTotalWidth * kMaxTotalWidth];
   uint64_t rcode;
   double margin;
   int ok;
@@ -2901,22 +2903,26 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     __syncthreads();
     phase(4);
     if (!S.ok) continue;
-    // ---- quad_decode: border gray models (8 patterns x 8 samples = 64 lanes) ----
+    // ---- quad_decode: border gray models (8 patterns x width_at_border <= 8
+    // samples: lane = 8 * pattern + sample) ----
+    const int wab = prm.fam.width_at_border, tw = prm.fam.total_width, nbits = prm.fam.nbits;
+    const int minc = (wab - tw) / 2;
     {
       const int pidx = tid >> 3, i = tid & 7;
-      const float* pat = c_border_pat[pidx];
-      const double tagx01 = (double)((pat[0] + (float)i * pat[2]) / 8.0f);
-      const double tagy01 = (double)((pat[1] + (float)i * pat[3]) / 8.0f);
+      float p0, p1, p2, p3;
+      border_pattern(pidx, (float)wab, p0, p1, p2, p3);
+      const double tagx01 = (double)((p0 + (float)i * p2) / (float)wab);
+      const double tagy01 = (double)((p1 + (float)i * p3) / (float)wab);
       const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
       double px, py;
       hproject(S.H, tagx, tagy, &px, &py);
       const int ix = (int)px, iy = (int)py;
       S.gmx[tid] = tagx;
       S.gmy[tid] = tagy;
-      S.gmvalid[tid] = !(ix < 0 || iy < 0 || ix >= g.W || iy >= g.H);
+      S.gmvalid[tid] = i < wab && !(ix < 0 || iy < 0 || ix >= g.W || iy >= g.H);
       S.gmv[tid] = S.gmvalid[tid] ? (double)gray[(size_t)iy * g.W + ix] : 0.0;
     }
-    for (int t = tid; t < 100; t += kDecodeThreads) S.values[t] = 0;
+    for (int t = tid; t < tw * tw; t += kDecodeThreads) S.values[t] = 0;
     __syncthreads();
     phase(5);
     // lane 0 builds and solves the white model, lane 1 the black one, each over
@@ -2952,9 +2958,9 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     __syncthreads();
     if (w00 - b00 < 0) continue;  // uniform
     phase(6);
-    if (tid < 36) {
-      const int bity = c_bity[tid], bitx = c_bitx[tid];
-      const double tagx01 = (bitx + 0.5) / 8, tagy01 = (bity + 0.5) / 8;
+    if (tid < nbits) {
+      const int bity = prm.fam.bity[tid], bitx = prm.fam.bitx[tid];
+      const double tagx01 = (bitx + 0.5) / wab, tagy01 = (bity + 0.5) / wab;
       const double tagx = 2 * (tagx01 - 0.5), tagy = 2 * (tagy01 - 0.5);
       double px, py;
       hproject(S.H, tagx, tagy, &px, &py);
@@ -2967,40 +2973,43 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
                          gray[(size_t)y2 * g.W + x1] * (1 - xx) * yy + gray[(size_t)y2 * g.W + x2] * xx * yy;
         const double bth = S.bC[0] * tagx + S.bC[1] * tagy + S.bC[2];
         const double wth = S.wC[0] * tagx + S.wC[1] * tagy + S.wC[2];
-        S.values[10 * (bity + 1) + bitx + 1] = v - (bth + wth) / 2.0;
+        S.values[tw * (bity - minc) + bitx - minc] = v - (bth + wth) / 2.0;
       }
     }
     __syncthreads();
     phase(7);
-    // sharpen (apriltag.c): each lane owns cells t, t+64
-    double shv[2];
-    for (int r = 0; r < 2; r++) {
+    // sharpen (apriltag.c) over the total_width^2 grid: each lane owns cells t, t+64, t+128
+    constexpr int kShR = (kMaxTotalWidth * kMaxTotalWidth + kDecodeThreads - 1) / kDecodeThreads;
+    double shv[kShR];
+#pragma unroll
+    for (int r = 0; r < kShR; r++) {
       const int t = tid + 64 * r;
       shv[r] = 0;
-      if (t < 100) {
-        const int y = t / 10, x = t % 10;
+      if (t < tw * tw) {
+        const int y = t / tw, x = t % tw;
         const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
         double acc = 0;
         for (int i = 0; i < 3; i++)
           for (int j = 0; j < 3; j++) {
-            if ((y + i - 1) < 0 || (y + i - 1) > 9 || (x + j - 1) < 0 || (x + j - 1) > 9) continue;
-            acc += S.values[(y + i - 1) * 10 + (x + j - 1)] * kern[i * 3 + j];
+            if ((y + i - 1) < 0 || (y + i - 1) > tw - 1 || (x + j - 1) < 0 || (x + j - 1) > tw - 1) continue;
+            acc += S.values[(y + i - 1) * tw + (x + j - 1)] * kern[i * 3 + j];
           }
         shv[r] = acc;
       }
     }
     __syncthreads();
-    for (int r = 0; r < 2; r++) {
+#pragma unroll
+    for (int r = 0; r < kShR; r++) {
       const int t = tid + 64 * r;
-      if (t < 100) S.values[t] = S.values[t] + prm.decode_sharpening * shv[r];
+      if (t < tw * tw) S.values[t] = S.values[t] + prm.decode_sharpening * shv[r];
     }
     __syncthreads();
     if (tid == 0) {
       float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
       uint64_t rcode = 0;
-      for (int i = 0; i < 36; i++) {
+      for (int i = 0; i < nbits; i++) {
         rcode = rcode << 1;
-        const double v = S.values[10 * (c_bity[i] + 1) + c_bitx[i] + 1];
+        const double v = S.values[tw * (prm.fam.bity[i] - minc) + prm.fam.bitx[i] - minc];
         if (v > 0) { white_score = (float)(white_score + v); white_cnt++; rcode |= 1; }
         else { black_score = (float)(black_score - v); black_cnt++; }
       }
@@ -3010,15 +3019,15 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
     __syncthreads();
     phase(8);
     // quick_decode_codeword: first rotation, then entry, within hamming <= 2
-    // (codes are >= 11 apart, so at most one entry matches a rotation)
+    // (codes are >= 5 apart, so at most one entry matches a rotation)
     uint32_t bc = 0xffffffffu;
     {
       uint64_t r[4];
       r[0] = S.rcode;
 #pragma unroll
-      for (int k = 1; k < 4; k++) r[k] = rotate90_36(r[k - 1]);
-      for (int ent = tid; ent < c_book.n; ent += kDecodeThreads) {
-        const uint64_t c = c_book.code[ent];
+      for (int k = 1; k < 4; k++) r[k] = rotate90_n(r[k - 1], nbits);
+      for (int ent = tid; ent < prm.fam.ncodes; ent += kDecodeThreads) {
+        const uint64_t c = b.book_code[ent];
 #pragma unroll
         for (int rot = 0; rot < 4; rot++) {
           const int hd = __popcll(r[rot] ^ c);
@@ -3033,7 +3042,7 @@ __global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Pa
       if (margin >= 0 && bc != 0xffffffffu) {
         const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
         DevDetection d;
-        d.id = c_book.id[ent];
+        d.id = b.book_id[ent];
         d.hamming = hd;
         d.decision_margin = margin;
         d.blob_rank = (int32_t)qrank;
@@ -3123,16 +3132,6 @@ hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint3
 // ---------------------------------------------------------------------------
 // launch helpers (called from at_api.cpp)
 // ---------------------------------------------------------------------------
-hipError_t upload_codebook(const uint64_t* codes, const int* ids, int n) {
-  DevCodebook cb;
-  cb.n = n;
-  if (n < 0 || n > kMaxCodes) return hipErrorInvalidValue;
-  for (int i = 0; i < n; i++) {
-    cb.code[i] = codes[i];
-    cb.id[i] = ids[i];
-  }
-  return hipMemcpyToSymbol(HIP_SYMBOL(c_book), &cb, sizeof(cb));
-}
 
 // Kernel order of one launch sequence; ev (optional, kNumStages+1 events)
 // brackets every kernel for per-stage timing.

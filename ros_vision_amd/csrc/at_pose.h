@@ -136,7 +136,13 @@ __device__ M3 polar3(M3 x) {
 
 // 1/sqrt(x), x > 0: the hardware estimate and one second-order correction
 // (y (1 + e/2 + 3e^2/8), e = 1 - x y^2) -- ocml's refinement without its
-// special-case select (x = 0 and inf do not reach the callers below)
+// special-case select.  x = 0 does reach it: polar_rank2_cols passes
+// D = max(ac - b^2, 0), which is 0 when the iterate's two columns are parallel
+// (all four image rays in one plane through the camera centre, i.e. collinear
+// corners).  Then rsq(0) = inf and the pose and its error come out NaN --
+// a documented outcome, not reachable from the pipeline:
+// UpdateFitQuads' area test (>= 0.95 * 4^2, apriltag_detect.cu:190-200) rejects
+// such quads before k_pose sees them.
 __device__ __forceinline__ double rsqrt_pos(double x) {
   const double y = __builtin_amdgcn_rsq(x);
   const double e = fma(-x * y, y, 1.0);

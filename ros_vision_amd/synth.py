@@ -1,10 +1,11 @@
-"""Seeded synthetic tag36h11 boards.
+"""Seeded synthetic tag boards (tag36h11 unless a
+family is named).
 
-A frame is a mid-gray background with ``ntags`` tag36h11 tags on a jittered
-grid; each tag gets a random side length, rotation and perspective
-(corner jitter), is rendered with bilinear interpolation from a 10x10-cell
-bitmap (white quiet zone, black border, 6x6 data cells in the apriltag 3.x
-bit layout) and the frame gets Gaussian noise.  Output is the gray plane or
+A frame is a mid-gray background with ``ntags`` tags on a jittered grid; each
+tag gets a random side length, rotation and perspective (corner jitter), is
+rendered with bilinear interpolation from a (d+4)x(d+4)-cell bitmap (white
+quiet zone, black border, d x d data cells in the apriltag 3.x bit layout; d = 6
+for tag36h11, 5 for tag25h9, 4 for tag16h5) and the frame gets Gaussian noise.  Output is the gray plane or
 packed YUYV with U = V = 128 (what cvtColor(BGR2YUV_YUYV) produces for a gray
 image, apriltags_cuda_detector.cu:401).  Stream frames (configs C2-C4) carry
 ids 10f .. 10f+ntags-1 mod 587, so a run of frames walks
@@ -16,14 +17,40 @@ import numpy as np
 BIT_X = [1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4, 1, 1, 1, 1, 1, 2, 2, 2, 3]
 BIT_Y = [1, 1, 1, 1, 1, 2, 2, 2, 3, 1, 2, 3, 4, 5, 2, 3, 4, 3, 6, 6, 6, 6, 6, 5, 5, 5, 4, 6, 5, 4, 3, 2, 5, 4, 3, 4]
 
+# data grid side of the classic families the detector supports
+FAMILY_D = {"tag36h11": 6, "tag25h9": 5, "tag16h5": 4}
 
-def tag_cells(code: int) -> np.ndarray:
-    """10x10 cell image (1 = white) of a tag36h11 codeword incl. the quiet zone."""
-    cells = np.ones((10, 10), np.float32)
-    cells[1:9, 1:9] = 0.0  # black border ring
-    for i in range(36):
-        if (code >> (35 - i)) & 1:
-            cells[BIT_Y[i] + 1, BIT_X[i] + 1] = 1.0
+
+def family_layout(family: str = "tag36h11"):
+    """3.x bit_x / bit_y of a classic family: the upper triangle of the top-left
+    quadrant row by row, rotated by 90 degrees three more times ((x, y) ->
+    (d+1-y, x)), the centre cell last for odd d."""
+    d = FAMILY_D[family]
+    xs, ys = [], []
+    for r in range(4):
+        for y in range(1, d // 2 + 1):
+            for x in range(y, d - y + 1):
+                xx, yy = x, y
+                for _ in range(r):
+                    xx, yy = d + 1 - yy, xx
+                xs.append(xx)
+                ys.append(yy)
+    if d % 2:
+        xs.append(d // 2 + 1)
+        ys.append(d // 2 + 1)
+    return xs, ys
+
+
+def tag_cells(code: int, family: str = "tag36h11") -> np.ndarray:
+    """(d+4)x(d+4) cell image (1 = white) of a codeword incl. the quiet zone."""
+    d = FAMILY_D[family]
+    n = d * d
+    bx, by = family_layout(family)
+    cells = np.ones((d + 4, d + 4), np.float32)
+    cells[1:d + 3, 1:d + 3] = 0.0  # black border ring
+    for i in range(n):
+        if (code >> (n - 1 - i)) & 1:
+            cells[by[i] + 1, bx[i] + 1] = 1.0
     return cells
 
 
@@ -37,21 +64,17 @@ def homography(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
     return Hm / Hm[2, 2]
 
 
-def _known_ids():
+def _codes(family: str = "tag36h11"):
     from .detector import family_entries  # codebook lives in the C library
-    return sorted(i for i, _ in family_entries())
-
-
-def _codes():
-    from .detector import family_entries
-    return dict(family_entries())
+    return dict(family_entries(family))
 
 
 def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigma: float = 2.0,
-                 side_range=(64, 128), ids=None, background: int = 128, codes=None):
+                 side_range=(64, 128), ids=None, background: int = 128, codes=None, family: str = "tag36h11"):
     """Render one gray frame; returns (gray uint8 [H,W], list of (id, corners[4,2]))."""
     rng = np.random.default_rng(seed)
-    codes = codes if codes is not None else _codes()
+    codes = codes if codes is not None else _codes(family)
+    nc = FAMILY_D[family] + 4  # cells across, quiet zone included
     known = sorted(codes)
     if ids is None:
         start = int(rng.integers(0, len(known)))
@@ -69,16 +92,16 @@ def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigm
         cx = (c + 0.5) * cw + rng.uniform(-0.08, 0.08) * cw
         cy = (r + 0.5) * ch + rng.uniform(-0.08, 0.08) * ch
         ang = np.deg2rad(rng.uniform(-10, 10))
-        # square of the full 10-cell tag (quiet zone included), then perspective jitter
-        half = side / 2 * 10 / 8
+        # square of the full tag (quiet zone included), then perspective jitter
+        half = side / 2 * nc / (nc - 2)
         base = np.array([[-half, -half], [half, -half], [half, half], [-half, half]])
         rot = np.array([[np.cos(ang), -np.sin(ang)], [np.sin(ang), np.cos(ang)]])
         corners = base @ rot.T + np.array([cx, cy])
         corners += rng.uniform(-0.15, 0.15, size=(4, 2)) * half * 0.5
-        src = np.array([[0, 0], [10, 0], [10, 10], [0, 10]], np.float64)
+        src = np.array([[0, 0], [nc, 0], [nc, nc], [0, nc]], np.float64)
         Hm = homography(src, corners)
         Hinv = np.linalg.inv(Hm)
-        bmp = np.kron(tag_cells(codes[tid]), np.ones((sup, sup), np.float32)) * 255.0
+        bmp = np.kron(tag_cells(codes[tid], family), np.ones((sup, sup), np.float32)) * 255.0
         x0, y0 = np.floor(corners.min(0)).astype(int) - 1
         x1, y1 = np.ceil(corners.max(0)).astype(int) + 1
         x0, y0, x1, y1 = max(x0, 0), max(y0, 0), min(x1, width - 1), min(y1, height - 1)
@@ -86,10 +109,10 @@ def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigm
         pts = np.stack([xs.ravel() + 0.5, ys.ravel() + 0.5, np.ones(xs.size)])
         tp = Hinv @ pts
         u, v = tp[0] / tp[2], tp[1] / tp[2]
-        inside = (u >= 0) & (u < 10) & (v >= 0) & (v < 10)
+        inside = (u >= 0) & (u < nc) & (v >= 0) & (v < nc)
         bu, bv = u * sup - 0.5, v * sup - 0.5
-        iu = np.clip(np.floor(bu).astype(int), 0, 10 * sup - 2)
-        iv = np.clip(np.floor(bv).astype(int), 0, 10 * sup - 2)
+        iu = np.clip(np.floor(bu).astype(int), 0, nc * sup - 2)
+        iv = np.clip(np.floor(bv).astype(int), 0, nc * sup - 2)
         fu = np.clip(bu - iu, 0, 1)
         fv = np.clip(bv - iv, 0, 1)
         val = (bmp[iv, iu] * (1 - fu) * (1 - fv) + bmp[iv, iu + 1] * fu * (1 - fv) +
@@ -97,8 +120,8 @@ def render_board(width: int, height: int, seed: int, ntags: int = 15, noise_sigm
         flat = img[y0:y1 + 1, x0:x1 + 1].ravel()
         flat[inside] = val[inside]
         img[y0:y1 + 1, x0:x1 + 1] = flat.reshape(ys.shape)
-        # tag black-border corners (cells 1 and 9) in image space
-        bc = np.array([[1, 1], [9, 1], [9, 9], [1, 9]], np.float64)
+        # tag black-border corners (cells 1 and nc-1) in image space
+        bc = np.array([[1, 1], [nc - 1, 1], [nc - 1, nc - 1], [1, nc - 1]], np.float64)
         hb = Hm @ np.vstack([bc.T, np.ones(4)])
         truth.append((tid, (hb[:2] / hb[2]).T))
     if noise_sigma > 0:

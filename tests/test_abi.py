@@ -58,7 +58,7 @@ def test_invalid_geometry_rejected_before_any_gpu_call():
         assert L.at_create(C.byref(cfg), C.byref(cam), C.byref(hnd)) == -1  # AT_E_INVALID
     cfg = detector.AtConfig()
     L.at_config_default(C.byref(cfg), 1280, 720)
-    cfg.family = b"tag25h9"
+    cfg.family = b"tagStandard41h12"  # named by setup_tag_family, no codebook offline
     assert L.at_create(C.byref(cfg), C.byref(cam), C.byref(C.c_void_p())) == -4  # AT_E_FAMILY
     assert L.at_strerror(-3) == b"frame exceeded a fixed capacity"
 

@@ -13,8 +13,9 @@ def test_oracle_reproduces_golden(name):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_golden_vectors as mg
-    case = {n: (W, H, fmt, frame) for n, W, H, fmt, frame in mg.cases()}[name]
+    case = {c[0]: c[1:] for c in mg.cases()}[name]
     got = mg.run_case(*case)
+    assert VEC[name].get("family", "tag36h11") == case[4]
     want = VEC[name]
     for k in got:
         assert got[k] == want[k], k

@@ -154,8 +154,8 @@ def test_gpu_matches_committed_golden(gpu, name):
     sys.path.insert(0, os.path.join(root, "tools"))
     import make_golden_vectors as mg
     want = _golden()[name]
-    W, H, fmt, frame = {n: (W, H, f, fr) for n, W, H, f, fr in mg.cases()}[name]
-    det = gpu.GpuDetector(W, H)
+    W, H, fmt, frame, family = {c[0]: c[1:] for c in mg.cases()}[name]
+    det = gpu.GpuDetector(W, H, family=family)
     dets = det.detect(frame, fmt)
     assert mg.digest(det.copy_thresholded()) == want["thr"]
     assert mg.digest(det.copy_union_markers()) == want["labels"]
