@@ -616,6 +616,26 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   }
 }
 
+// Once every count has reached its root: each local root's parent word becomes
+// root | kept << 31 (kept: the component has >= 25 pixels, the BlobDiff size
+// test, apriltag_gpu.cu:331-337), so k_boundary reads label and size test in the
+// same two hops and never touches the size plane.
+constexpr uint32_t kKeptBit = 0x80000000u;
+__global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
+  const int f = blockIdx.y;
+  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
+  const size_t fo = (size_t)f * g.Wd * g.Hd;
+  uint32_t* par = b.par + fo;
+  const uint32_t* size = b.size + fo;
+  const uint32_t n = b.nlroot[tl];
+  const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
+  for (uint32_t k = threadIdx.x; k < n; k += 64) {
+    const uint32_t l = lr[k];
+    const uint32_t r = par[l];
+    par[l] = r | (size[r] >= 25 ? kKeptBit : 0u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K6: boundary points (BlobDiff) fused with stream compaction and the pair
 // histogram.  Points are appended with one atomic per wave per direction; the
@@ -723,39 +743,43 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   const uint8_t* thr = b.thr + fo;
   const uint32_t* par = b.par + fo;
-  const uint32_t* size = b.size + fo;
   const int Wd = g.Wd;
   const int ty0 = 1 + blockIdx.y * (4 * kBndRows), tx0 = blockIdx.x * 64;  // halo origin: x0 - 1
   constexpr int kTR = 4 * kBndRows + 1, kTC = 66, kTN = kTR * kTC;
   constexpr int kPer = (kTN + 255) / 256;
   // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
-  // column) -> local root -> component root (k_ccl_roots)
-  uint32_t lv[kPer];
+  // column) -> local root -> component root | kept bit (k_ccl_roots, k_ccl_keep;
+  // a local root's own word already holds root | kept, so the second hop masks)
+  // (the threshold byte and both candidate nodes' parents are loaded together,
+  // the byte then picks fg or bg: one round trip fewer than thr -> node -> parent)
+  uint32_t lv[kPer], lb[kPer];
   uint8_t tv[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
     lv[k] = 0xffffffffu;
+    lb[k] = 0xffffffffu;
     tv[k] = 127;
     if (e < kTN && yy < g.Hd && xx < Wd) {
       const size_t i = (size_t)yy * Wd + xx;
-      const uint32_t v = thr[i];
-      tv[k] = (uint8_t)v;
+      tv[k] = thr[i];
       const uint32_t F = (uint32_t)((yy & ~1) * Wd + (xx & ~1));
-      const uint32_t node = v == 255 ? F : F + Wd + (xx & 1);
-      if (v != 127) lv[k] = par[node];
+      lv[k] = par[F];
+      lb[k] = par[F + Wd + (xx & 1)];
     }
   }
 #pragma unroll
-  for (int k = 0; k < kPer; k++)
-    if (lv[k] != 0xffffffffu) lv[k] = par[lv[k]];
+  for (int k = 0; k < kPer; k++) {
+    lv[k] = tv[k] == 127 ? 0xffffffffu : (tv[k] == 255 ? lv[k] : lb[k]);
+    if (lv[k] != 0xffffffffu) lv[k] = par[lv[k] & ~kKeptBit];
+  }
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     if (e < kTN) {
-      const bool kept = lv[k] != 0xffffffffu && size[lv[k]] >= 25;
-      s_tlab[e] = lv[k];
+      const bool kept = lv[k] != 0xffffffffu && (lv[k] & kKeptBit);
+      s_tlab[e] = lv[k] & ~kKeptBit;
       s_tthr[e] = kept ? tv[k] : (uint8_t)127;
     }
   }
@@ -3095,7 +3119,7 @@ __global__ __launch_bounds__(256) void k_tap_sizes(const uint8_t* thr, const uin
   } else {
     has = thr[i] == 0 || thr[i - Wd] == 0;  // the block's column of this bg node
   }
-  if (node && has && par[i] == (uint32_t)i) v = size[i];
+  if (node && has && (par[i] & ~kKeptBit) == (uint32_t)i) v = size[i];
   out[i] = v;
 }
 
@@ -3113,7 +3137,7 @@ __global__ __launch_bounds__(256) void k_tap_labels(const uint8_t* thr, const ui
   uint32_t lab;
   if (all127) lab = (uint32_t)i;
   else if (thr[i] == 127) lab = 0;
-  else lab = par[par[thr[i] == 255 ? F : F + Wd + (x & 1)]];
+  else lab = par[par[thr[i] == 255 ? F : F + Wd + (x & 1)] & ~kKeptBit] & ~kKeptBit;
   out[i] = lab;
 }
 
@@ -3220,7 +3244,10 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     mark();
   }
   tk(3, st, 0);
-  if (on(3)) hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+  if (on(3)) {
+    hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+    hipLaunchKernelGGL(k_ccl_keep, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+  }
   tk(3, st, 1);
   mark();
   {
