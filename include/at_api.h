@@ -49,7 +49,8 @@ typedef struct {
  * (apriltags_cuda_detector.cu:139-147; apriltag_gpu.cu:166-181, 737, 884, 1084-1086). */
 typedef struct {
   int width, height;          /* frame size; width%8==0, height%8==0, width*height < 2^22 */
-  const char *family;         /* "tag36h11" (apriltags_cuda_detector.hpp:213) */
+  const char *family;         /* "tag36h11" (apriltags_cuda_detector.hpp:213), "tag25h9", "tag16h5";
+                                 the apriltag 3 layouts give AT_E_FAMILY (apriltag_utils.cu:10-32) */
   float quad_decimate;        /* must be 2.0 (apriltag_gpu.cu:166) */
   int refine_edges;           /* 1 */
   double decode_sharpening;   /* 0.25 */
@@ -195,6 +196,22 @@ typedef struct {
 } at_tag_detection;
 int at_tag_detections(const at_pose *poses, int n, const double *extr_R, const double *extr_t,
                       at_tag_detection *out);
+
+/* Shared game-piece preprocessing: the network input of
+ * preprocess_image (src/game_piece_detection/src/game_piece_detection_node.cu:347-379:
+ * cv::resize INTER_LINEAR to out_width x out_height, BGR->RGB for 3 channels or
+ * BGR->GRAY for 1, x 1/255, NCHW float) computed on the GPU from the same BGR8
+ * frames the detector reads.  at_gp_enable adds it to the launch sequence (every
+ * later batch of AT_FMT_BGR8 frames); at_gp_tensor gives frame `frame`'s tensor of
+ * the last batch in device memory (channels x out_height x out_width floats, valid
+ * until the next batch); at_gp_copy copies it to the host.  AT_E_INVALID when the
+ * last batch was not BGR8.  at_gp_preprocess_device runs it standalone on one
+ * device-resident BGR8 image on `stream` (a hipStream_t, NULL = default stream). */
+int at_gp_enable(at_detector *d, int out_width, int out_height, int channels);
+int at_gp_tensor(at_detector *d, int frame, const float **dev_ptr);
+int at_gp_copy(at_detector *d, int frame, float *dst, size_t count);
+int at_gp_preprocess_device(const uint8_t *bgr, int width, int height, float *out, int out_width, int out_height,
+                            int channels, void *stream);
 
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);

@@ -91,6 +91,7 @@ def lib():
         L.ao_rotate90.argtypes = [C.c_uint64]
         L.ao_unrank.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
         L.ao_set_fp_perturb.argtypes = [C.c_int]
+        L.ao_gp_preprocess.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
         _LIB = L
     return _LIB
 
@@ -235,3 +236,16 @@ def family_layout(family="tag36h11"):
         xs.append(x.value)
         ys.append(y.value)
     return xs, ys
+
+
+def gp_preprocess(bgr: np.ndarray, out_width=640, out_height=640, channels=3):
+    """preprocess_image (game_piece_detection_node.cu:347-379) restated in ao_gp.c:
+    (channels, out_height, out_width) float32."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w, c = bgr.shape
+    assert c == 3
+    out = np.empty((channels, out_height, out_width), np.float32)
+    rc = lib().ao_gp_preprocess(bgr.ctypes.data, w, h, out.ctypes.data, out_width, out_height, channels)
+    if rc != 0:
+        raise ValueError("ao_gp_preprocess: invalid arguments")
+    return out

@@ -119,6 +119,10 @@ float ao_det_hypotf(float a, float b);
 int ao_estimate_tag_pose(const double H[9], const double corners[4][2], double fx, double fy, double cx, double cy,
                          double tagsize, double R[9], double t[3], double err[2]);
 
+/* shared game-piece preprocessing (ao_gp.c; preprocess_image of
+ * game_piece_detection_node.cu:347-379): bgr h x w x 3 -> out channels x oh x ow */
+int ao_gp_preprocess(const uint8_t *bgr, int w, int h, float *out, int ow, int oh, int channels);
+
 /* helpers exposed for tests */
 uint64_t ao_rotate90(uint64_t w);                 /* 36 bits */
 uint64_t ao_rotate90_n(uint64_t w, int nbits);

@@ -24,6 +24,7 @@ namespace at {
 hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint32_t* size, uint32_t* out, int Wd,
                             int Hd, hipStream_t st);
 hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd, hipStream_t st);
+hipError_t launch_gp_preprocess(const uint8_t* src, int w, int h, float* out, int ow, int oh, int c, hipStream_t st);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt);
@@ -137,6 +138,7 @@ struct at_detector {
   std::vector<at_pose> poses;   // [B][kMaxDets] poses of the last collected batch (id order)
   std::vector<int> nposes;      // [B]
   int last_nframes;
+  int last_fmt;
   int pending;
   hipEvent_t ev_done;
   hipEvent_t ev_ext;                      // at_stream_wait: recorded on the producer's stream
@@ -641,6 +643,7 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   }
   HIPCHK(hipEventRecord(d->ev_done, st));
   d->last_nframes = nframes;
+  d->last_fmt = fmt;
   d->pending = 1;
   return AT_OK;
 }
@@ -840,6 +843,67 @@ int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const d
                    [](const at_tag_detection& a, const at_tag_detection& b) { return a.distance < b.distance; });
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
+}
+
+// ---- shared game-piece preprocessing ---------------------
+static void drop_graphs(at_detector* d) {
+  for (auto& kv : d->graphs) (void)hipGraphExecDestroy(kv.second);
+  d->graphs.clear();
+  for (auto& kv : d->split_graphs)
+    for (auto* g : kv.second.seg) (void)hipGraphExecDestroy(g);
+  d->split_graphs.clear();
+}
+
+int at_gp_enable(at_detector* d, int out_width, int out_height, int channels) {
+  if (!d || out_width < 1 || out_height < 1 || out_width > 8192 || out_height > 8192 ||
+      (channels != 1 && channels != 3))
+    return AT_E_INVALID;
+  if (hipSetDevice(d->device) != hipSuccess) return AT_E_HIP;
+  if (d->pending && hipEventSynchronize(d->ev_done) != hipSuccess) return AT_E_HIP;
+  const size_t bytes = (size_t)d->B * channels * out_width * out_height * sizeof(float);
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return AT_E_NOMEM;
+  if (d->d.gp_out) {
+    for (auto& a : d->allocs)
+      if (a == d->d.gp_out) a = nullptr;
+    (void)hipFree(d->d.gp_out);
+  }
+  d->allocs.push_back(p);
+  d->d.gp_out = (float*)p;
+  d->prm.gp_w = out_width;
+  d->prm.gp_h = out_height;
+  d->prm.gp_c = channels;
+  drop_graphs(d);  // the captured sequences carry the old parameters
+  return AT_OK;
+}
+
+int at_gp_tensor(at_detector* d, int frame, const float** dev_ptr) {
+  if (!d || !dev_ptr || !d->prm.gp_c || frame < 0 || frame >= d->last_nframes || d->last_fmt != AT_FMT_BGR8)
+    return AT_E_INVALID;
+  *dev_ptr = d->d.gp_out + (size_t)frame * d->prm.gp_c * d->prm.gp_w * d->prm.gp_h;
+  return AT_OK;
+}
+
+int at_gp_copy(at_detector* d, int frame, float* dst, size_t count) {
+  const float* src = nullptr;
+  const int rc = at_gp_tensor(d, frame, &src);
+  if (rc != AT_OK) return rc;
+  const size_t n = (size_t)d->prm.gp_c * d->prm.gp_w * d->prm.gp_h;
+  if (!dst || count < n) return AT_E_INVALID;
+  if (hipSetDevice(d->device) != hipSuccess) return AT_E_HIP;
+  if (d->pending && hipEventSynchronize(d->ev_done) != hipSuccess) return AT_E_HIP;
+  return hipMemcpy(dst, src, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? AT_OK : AT_E_HIP;
+}
+
+int at_gp_preprocess_device(const uint8_t* bgr, int width, int height, float* out, int out_width, int out_height,
+                            int channels, void* stream) {
+  if (!bgr || !out || width < 2 || height < 2 || out_width < 1 || out_height < 1 || out_width > 8192 ||
+      out_height > 8192 || (channels != 1 && channels != 3))
+    return AT_E_INVALID;
+  return launch_gp_preprocess(bgr, width, height, out, out_width, out_height, channels, (hipStream_t)stream) ==
+                 hipSuccess
+             ? AT_OK
+             : AT_E_HIP;
 }
 
 int at_frame_status(at_detector* d, int frame) {

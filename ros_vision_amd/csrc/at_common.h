@@ -121,6 +121,7 @@ struct Params {
   int wide_blob;  // AT_WIDE_BLOB=1: 512-thread large-blob teams at every batch size (experiment)
   int pipe_stop;  // diagnostics only (AT_DIAG_PIPE_STOP): launch the stages < N only; 0 = all
   FamilyDesc fam;
+  int gp_w, gp_h, gp_c;  // game-piece preprocessing output (at_gp_enable); gp_c == 0: off
 };
 constexpr int kProbeWords = 256;
 
@@ -222,6 +223,7 @@ struct DevBufs {
   double* rsamp;      // [decode workgroups][2][kMaxRefineSamples - kLdsRefine] refine samples past LDS
   const uint64_t* book_code;  // [fam.ncodes] codebook (3.x bit order)
   const int32_t* book_id;     // [fam.ncodes] tag id of each code
+  float* gp_out;              // [B][gp_c][gp_h][gp_w] game-piece network input (at_gp_enable)
   // per-workgroup scratch of the blob kernel
   uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
                       // (pathological blobs only; every other per-blob array lives in LDS)

@@ -896,6 +896,14 @@ __device__ void block_bitonic_sort(T* s, int n) {
   }
 }
 
+// k_pairs turns the first kGrpEnt entries of every tile into the base slot of
+// the tile's points in their pair segment (written over the entry's count), so
+// k_group scatters a tile with one load round trip; kGrpDrop marks pairs outside
+// the size bounds, kGrpFallback entries whose points reserve one slot each.
+constexpr int kGrpEnt = 128;  // tile entries with an LDS cursor in k_group (typical tiles: ~10)
+constexpr uint32_t kGrpDrop = 0xfffffffeu, kGrpFallback = 0xffffffffu;
+constexpr int kPairsEntCache = 4;  // entries per thread whose hash slot k_pairs keeps in registers
+
 __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
@@ -916,48 +924,63 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __syncthreads();
   // merge the per-tile pair histograms of k_boundary in LDS: wave w takes
   // tiles w, w + 16, ...; then the overflow entries of crowded tiles
-  auto merge = [&](uint64_t key, uint32_t cnt) {
-    uint32_t h = (uint32_t)mix_hash(key);
-    bool done = false;
-    for (int probe = 0; probe < kHashSlots && !done; probe++) {
+  auto merge = [&](uint64_t key, uint32_t cnt) -> uint32_t {
+    uint32_t h = (uint32_t)mix_hash(key) & (kHashSlots - 1);
+    for (int probe = 0; probe < kHashSlots; probe++) {
       const uint64_t k = t_key[h];
       if (k == key) {
         atomicAdd(&t_cnt[h], cnt);
-        done = true;
+        return h;
       } else if (k == 0) {
         const uint64_t prev = atomicCAS((unsigned long long*)&t_key[h], 0ull, (unsigned long long)key);
         if (prev == 0 || prev == key) {
           atomicAdd(&t_cnt[h], cnt);
-          done = true;
+          return h;
         }
       }
       h = (h + 1) & (kHashSlots - 1);
     }
-    if (!done) s_full = 1;
+    s_full = 1;
+    return 0xffffffffu;
   };
+  // the first kPairsEntCache * 1024 tile entries of the flat pass: hash slot,
+  // count and global index (for the segment bases written at the end)
+  uint32_t c_slot[kPairsEntCache], c_cnt[kPairsEntCache], c_idx[kPairsEntCache];
+  bool c_lds[kPairsEntCache];
+#pragma unroll
+  for (int k = 0; k < kPairsEntCache; k++) { c_slot[k] = 0xffffffffu; c_cnt[k] = 0; c_idx[k] = 0; c_lds[k] = false; }
+  __shared__ uint32_t s_tpre[kMaxTilesPerFrame + 1];
+  uint32_t tot_e = 0;
   {
     // tile entry counts -> exclusive prefix in LDS (one load round trip), then
     // every entry of the frame in one flat pass
-    __shared__ uint32_t s_tpre[kMaxTilesPerFrame + 1];
     const int ntb = g.ntb;
     // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
     const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
     const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
-    uint32_t tot_e;
     const uint32_t incl_e = block_incl_scan(ne, s_wsum, &tot_e, 16);
     if (tid < ntb) s_tpre[tid] = incl_e - ne;
     if (tid == 0) s_tpre[ntb] = tot_e;
     if (np) atomicAdd(&s_np, np);
     __syncthreads();
-    for (uint32_t i = tid; i < tot_e; i += 1024) {
+    for (uint32_t i = tid, k = 0; i < tot_e; i += 1024, k++) {
       int lo = 0, hi = ntb - 1;  // last tile whose prefix <= i
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (s_tpre[mid] <= i) lo = mid;
         else hi = mid - 1;
       }
-      const size_t e = ((size_t)f * ntb + lo) * kLdsPairSlots + (i - s_tpre[lo]);
-      merge(b.pent_key[e], b.pent_cnt[e]);
+      const uint32_t et = i - s_tpre[lo];
+      const size_t e = ((size_t)f * ntb + lo) * kLdsPairSlots + et;
+      const uint32_t cnt = b.pent_cnt[e];
+      const uint32_t slot = merge(b.pent_key[e], cnt);
+      if (k < (uint32_t)kPairsEntCache) {
+#pragma unroll
+        for (int kk = 0; kk < kPairsEntCache; kk++)  // (constant register indices)
+          if (kk == (int)k) { c_slot[kk] = slot; c_cnt[kk] = cnt; c_idx[kk] = (uint32_t)e; c_lds[kk] = et < (uint32_t)kGrpEnt; }
+      } else if (et < (uint32_t)kGrpEnt) {
+        b.pent_cnt[e] = kGrpFallback;  // beyond the register cache: k_group reserves per point
+      }
     }
     const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
     for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
@@ -1055,12 +1078,43 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
       b.ht_rank[(size_t)f * kHashSlots + slot] = (uint32_t)i;
       b.ht_off[(size_t)f * kHashSlots + slot] = offs[k];
-      b.ht_cur[(size_t)f * kHashSlots + slot] = 0;
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
       b.pair_off[(size_t)f * kMaxPairs + i] = offs[k];
       b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
       if (cls[k] >= 0)
         b.work[(size_t)cls[k] * b.wcap + s_cbase[cls[k]] + lslot[k]] = ((uint32_t)f << 16) | (uint32_t)i;
+    }
+  }
+  // segment bases of the tiles' first kGrpEnt entries (LDS cursors per pair slot;
+  // t_key's storage is free since the sort), then the cursors' final values seed
+  // k_group's per-point reservations
+  uint32_t* t_off = reinterpret_cast<uint32_t*>(t_key);
+  uint32_t* t_cur = t_off + kHashSlots;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + k;
+    if (i < (int)n) {
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      t_off[slot] = offs[k];
+      t_cur[slot] = 0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPairsEntCache; k++) {
+    if (c_slot[k] != 0xffffffffu && c_lds[k]) {
+      const uint32_t tc = t_cnt[c_slot[k]];
+      const bool keep = tc >= g.min_cluster && tc <= g.max_cluster;
+      b.pent_cnt[c_idx[k]] = keep ? t_off[c_slot[k]] + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + k;
+    if (i < (int)n) {
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      b.ht_cur[(size_t)f * kHashSlots + slot] = t_cur[slot];
     }
   }
   stamp(5);
@@ -1069,56 +1123,60 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 // ---------------------------------------------------------------------------
 // K8: scatter the points into their pair segments (grouped by pair rank).
 // ---------------------------------------------------------------------------
-// One workgroup per k_boundary tile: every (tile, pair) entry reserves its
-// points' range of the pair segment with one atomic, then the tile's points
-// take consecutive slots of their entry (LDS cursor).  Pairs missing from the
-// tile's entries (LDS table overflow in k_boundary) reserve per point.
-constexpr int kGrpEnt = 128;  // tile entries with an LDS cursor (typical tiles: ~10)
+// One workgroup per k_boundary tile.  k_pairs has reserved each of the tile's
+// first kGrpEnt (tile, pair) entries its range of the pair segment (the entry's
+// count word now holds the base, kGrpDrop for pairs outside SelectBlobs' count
+// bounds -- P4's size filter: nothing reads their segments); the tile's points
+// take consecutive slots of their entry's range (LDS cursor).  The tile's
+// counters, its entries and its first 1024 points are loaded in ONE round trip
+// (speculatively: reads past the counts stay inside the tile's regions).  Points
+// of later entries (crowded tiles) and of pairs missing from the tile's entries
+// (LDS table overflow in k_boundary) reserve one slot each.
+constexpr int kGrpPre = 4;  // points per thread loaded up front (kBndStage = 1024 per tile)
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const int f = blockIdx.y;
-  if (b.status[f] & (kStatusPairsOverflow | kStatusHashFull)) return;
-  // the tile's first kGrpEnt pair entries: an LDS table (<= 50 % full) mapping the
-  // pair key to the entry, whose points take consecutive slots of the range the
-  // entry reserved with one atomic; the points of later entries (crowded tiles)
-  // reserve one slot each.  Points of pairs outside SelectBlobs' count bounds
-  // (P4's size filter) are dropped: nothing reads their segments.
   __shared__ uint64_t s_hk[2 * kGrpEnt];
   __shared__ uint32_t s_he[2 * kGrpEnt];
   __shared__ uint32_t s_base[kGrpEnt], s_cur[kGrpEnt];
   const int tid = threadIdx.x;
   const size_t tb = (size_t)f * g.ntb + blockIdx.x;
+  const uint64_t* pts = b.pts + tb * g.bnd_region;
+  // one round trip: status, counters, entry, points
+  const uint32_t st = b.status[f];
   const uint32_t n = b.tcnt[tb], ne = b.tent[tb];
+  uint64_t ekey = 0;
+  uint32_t ebase = kGrpFallback;
+  if (tid < kGrpEnt) {
+    ekey = b.pent_key[tb * kLdsPairSlots + tid];
+    ebase = b.pent_cnt[tb * kLdsPairSlots + tid];
+  }
+  uint64_t pv[kGrpPre];
+#pragma unroll
+  for (int k = 0; k < kGrpPre; k++) pv[k] = pts[tid + 256 * k];
+  if (st & (kStatusPairsOverflow | kStatusHashFull)) return;
   const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
   const uint32_t* ht_off = b.ht_off + (size_t)f * kHashSlots;
   const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
   uint32_t* ht_cur = b.ht_cur + (size_t)f * kHashSlots;
-  constexpr uint32_t kDrop = 0xfffffffeu;
   auto in_bounds = [&](uint32_t c) { return c >= g.min_cluster && c <= g.max_cluster; };
   for (int i = tid; i < 2 * kGrpEnt; i += 256) s_hk[i] = 0;
   __syncthreads();
-  for (uint32_t e = tid; e < ne && e < (uint32_t)kGrpEnt; e += 256) {
-    const uint64_t key = b.pent_key[tb * kLdsPairSlots + e];
-    const uint32_t cnt = b.pent_cnt[tb * kLdsPairSlots + e];
-    const uint32_t slot = ht_slot_find(ht_key, key);
-    uint32_t base = 0;
-    if (slot != 0xffffffffu) base = in_bounds(ht_cnt[slot]) ? ht_off[slot] + atomicAdd(ht_cur + slot, cnt) : kDrop;
-    s_base[e] = base;
-    s_cur[e] = 0;
-    uint32_t h = (uint32_t)(mix_hash(key) & (2 * kGrpEnt - 1));
+  if (tid < kGrpEnt && (uint32_t)tid < ne && ebase != kGrpFallback) {
+    s_base[tid] = ebase;
+    s_cur[tid] = 0;
+    uint32_t h = (uint32_t)(mix_hash(ekey) & (2 * kGrpEnt - 1));
     while (true) {  // keys are distinct and the table is at most half full
-      const uint64_t prev = atomicCAS((unsigned long long*)&s_hk[h], 0ull, (unsigned long long)key);
+      const uint64_t prev = atomicCAS((unsigned long long*)&s_hk[h], 0ull, (unsigned long long)ekey);
       if (prev == 0) {
-        s_he[h] = e;
+        s_he[h] = (uint32_t)tid;
         break;
       }
       h = (h + 1) & (2 * kGrpEnt - 1);
     }
   }
   __syncthreads();
-  const uint64_t* pts = b.pts + tb * g.bnd_region;
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
-  for (uint32_t i = tid; i < n; i += 256) {
-    const uint64_t key = pts[i];
+  auto place = [&](uint64_t key) {
     const uint64_t r01 = key >> 24;
     uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
     uint32_t e = 0xffffffffu;
@@ -1129,14 +1187,18 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
       h = (h + 1) & (2 * kGrpEnt - 1);
     }
     if (e != 0xffffffffu) {
-      if (s_base[e] == kDrop) continue;
+      if (s_base[e] == kGrpDrop) return;
       grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = key;
     } else {
       const uint32_t slot = ht_slot_find(ht_key, r01);
-      if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) continue;
+      if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) return;
       grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = key;
     }
-  }
+  };
+#pragma unroll
+  for (int k = 0; k < kGrpPre; k++)
+    if ((uint32_t)(tid + 256 * k) < n) place(pv[k]);
+  for (uint32_t i = tid + 256 * kGrpPre; i < n; i += 256) place(pts[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -3193,6 +3255,98 @@ __global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Shared game-piece preprocessing: preprocess_image of
+// src/game_piece_detection/src/game_piece_detection_node.cu:347-379 --
+// cv::resize (INTER_LINEAR, 8UC3), BGR->RGB (3 channels) or BGR->GRAY (1),
+// convertTo(CV_32F, 1/255), HWC->CHW -- from the BGR frame in HBM, one thread per
+// output pixel.  The 8-bit arithmetic is OpenCV 4.9's (imgproc resize.cpp):
+//   both scales exactly 2: INTER_AREA's fast path, (s00 + s01 + s10 + s11 + 2) >> 2;
+//   else fx = (float)((dx + 0.5) * scale_x - 0.5), sx = floor(fx), fx -= sx, with
+//   sx < 0 -> (0, 0) and, from the first column with sx + 1 >= w on, S[sx] * 2048
+//   alone (sx >= w - 1 -> (w - 1, 0)); coefficients saturate_cast<short>(c * 2048)
+//   (round half even); rows sy, sy + 1 clamped to [0, h - 1];
+//   H = S[sx] a0 + S[sx + 3] a1;  v = (((b0 (H0 >> 4)) >> 16) + ((b1 (H1 >> 4)) >> 16) + 2) >> 2;
+//   gray Y = (1868 B + 9617 G + 4899 R + 8192) >> 14;  out = (float)v * (float)(1 / 255).
+// Restated in oracle/ao_gp.c (parity unpinned against OpenCV itself: no fixture).
+// ---------------------------------------------------------------------------
+struct GpGeom {
+  int w, h, ow, oh, c;
+  double sx, sy;  // scale_x, scale_y
+  int area2;      // both scales exactly 2
+};
+__device__ __forceinline__ int gp_coef(float c) { return (int)__builtin_rintf(c * 2048.f); }
+
+__device__ __forceinline__ void gp_pixel(const uint8_t* src, const GpGeom& q, int dx, int dy, float* out) {
+  int v[3];
+  if (q.area2) {
+    const uint8_t* s0 = src + ((size_t)(2 * dy) * q.w + 2 * dx) * 3;
+    const uint8_t* s1 = s0 + (size_t)q.w * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) v[c] = (s0[c] + s0[c + 3] + s1[c] + s1[c + 3] + 2) >> 2;
+  } else {
+    float fx = (float)((dx + 0.5) * q.sx - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0.f; sx = 0; }
+    const bool one = sx + 1 >= q.w;
+    if (one && sx >= q.w - 1) { fx = 0.f; sx = q.w - 1; }
+    const int a0 = gp_coef(1.f - fx), a1 = gp_coef(fx);
+    float fy = (float)((dy + 0.5) * q.sy - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int b0 = gp_coef(1.f - fy), b1 = gp_coef(fy);
+    const int r0 = min(max(sy, 0), q.h - 1), r1 = min(max(sy + 1, 0), q.h - 1);
+    const uint8_t* S0 = src + ((size_t)r0 * q.w + sx) * 3;
+    const uint8_t* S1 = src + ((size_t)r1 * q.w + sx) * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const int h0 = one ? S0[c] * 2048 : S0[c] * a0 + S0[c + 3] * a1;
+      const int h1 = one ? S1[c] * 2048 : S1[c] * a0 + S1[c + 3] * a1;
+      v[c] = (((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2;
+    }
+  }
+  const float a = (float)(1.0 / 255.0);
+  const size_t plane = (size_t)q.ow * q.oh, i = (size_t)dy * q.ow + dx;
+  if (q.c == 3) {  // BGR -> RGB planes
+    out[i] = (float)v[2] * a;
+    out[plane + i] = (float)v[1] * a;
+    out[2 * plane + i] = (float)v[0] * a;
+  } else {
+    out[i] = (float)((v[0] * 1868 + v[1] * 9617 + v[2] * 4899 + (1 << 13)) >> 14) * a;
+  }
+}
+
+__device__ __forceinline__ GpGeom gp_geom(int w, int h, int ow, int oh, int c) {
+  GpGeom q;
+  q.w = w; q.h = h; q.ow = ow; q.oh = oh; q.c = c;
+  q.sx = 1. / ((double)ow / w);
+  q.sy = 1. / ((double)oh / h);
+  q.area2 = q.sx == 2.0 && q.sy == 2.0;  // |scale - 2| < DBL_EPSILON <=> == 2 near 2
+  return q;
+}
+
+// in the launch sequence (frames of the batch through the frame table)
+__global__ __launch_bounds__(256) void k_gp_pre(DevBufs b, Geom g, Params prm) {
+  const int f = blockIdx.z;
+  const int dx = blockIdx.x * 64 + threadIdx.x, dy = blockIdx.y * 4 + threadIdx.y;
+  if (dx >= prm.gp_w || dy >= prm.gp_h) return;
+  const GpGeom q = gp_geom(g.W, g.H, prm.gp_w, prm.gp_h, prm.gp_c);
+  gp_pixel(b.frames[f], q, dx, dy, b.gp_out + (size_t)f * prm.gp_c * prm.gp_w * prm.gp_h);
+}
+
+// standalone (at_gp_preprocess_device)
+__global__ __launch_bounds__(256) void k_gp_pre_one(const uint8_t* src, int w, int h, float* out, int ow, int oh, int c) {
+  const int dx = blockIdx.x * 64 + threadIdx.x, dy = blockIdx.y * 4 + threadIdx.y;
+  if (dx >= ow || dy >= oh) return;
+  gp_pixel(src, gp_geom(w, h, ow, oh, c), dx, dy, out);
+}
+
+hipError_t launch_gp_preprocess(const uint8_t* src, int w, int h, float* out, int ow, int oh, int c, hipStream_t st) {
+  hipLaunchKernelGGL(k_gp_pre_one, dim3((ow + 63) / 64, (oh + 3) / 4), dim3(64, 4), 0, st, src, w, h, out, ow, oh, c);
+  return hipGetLastError();
+}
+
 // st2/fork/join: a second stream on which the small-blob kernel runs beside
 // the large-blob one (both read k_group's output, neither reads the other's);
 // with stage profiling (ev != nullptr) everything stays on st, in order.
@@ -3226,6 +3380,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
     else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
     tk(0, st, 1);
+    // game-piece network input from the same BGR frames (counted in stage 0's time)
+    if (on(0) && prm.gp_c && fmt == 1)
+      hipLaunchKernelGGL(k_gp_pre, dim3((prm.gp_w + 63) / 64, (prm.gp_h + 3) / 4, B), dim3(64, 4), 0, st, b, g, prm);
   }
   mark();
   {

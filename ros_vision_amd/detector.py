@@ -32,6 +32,7 @@ EXPORTS = [
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
+    "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -176,8 +177,22 @@ def load_library(path: str = LIB_PATH):
     L.at_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     L.at_tag_detections.argtypes = [C.POINTER(AtPose), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                     C.POINTER(AtTagDetection)]
+    if hasattr(L, "at_gp_enable"):  # (A/B builds of older sources lack it)
+        L.at_gp_enable.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.at_gp_tensor.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.at_gp_copy.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
+        L.at_gp_preprocess_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                              C.c_void_p]
     _LIB = L
     return L
+
+
+def game_piece_preprocess_device(bgr_ptr: int, width: int, height: int, out_ptr: int, out_width: int = 640,
+                                 out_height: int = 640, channels: int = 3, stream: int = 0):
+    """at_gp_preprocess_device: preprocess_image of one device-resident BGR8 image
+    into a device NCHW float buffer, enqueued on `stream` (hipStream_t handle)."""
+    _check(load_library().at_gp_preprocess_device(bgr_ptr, width, height, out_ptr, out_width, out_height, channels,
+                                                  stream or None), "at_gp_preprocess_device")
 
 
 def family_entries(family: str = "tag36h11"):
@@ -395,6 +410,25 @@ class GpuDetector:
 
     def frame_status(self, frame=0):
         return load_library().at_frame_status(self._h, frame)
+
+    # ---- shared game-piece preprocessing (game_piece_detection_node.cu:347-379) ----
+    def enable_game_piece_input(self, width=640, height=640, channels=3):
+        """Also produce preprocess_image's NCHW float tensor of every BGR8 frame
+        (resize INTER_LINEAR, BGR->RGB / GRAY, x 1/255) in each later batch."""
+        _check(load_library().at_gp_enable(self._h, width, height, channels), "at_gp_enable")
+        self._gp = (channels, height, width)
+
+    def game_piece_tensor_ptr(self, frame=0):
+        """Device pointer of frame `frame`'s tensor of the last (BGR8) batch."""
+        ptr = C.c_void_p()
+        _check(load_library().at_gp_tensor(self._h, frame, C.byref(ptr)), "at_gp_tensor")
+        return ptr.value
+
+    def game_piece_tensor(self, frame=0):
+        """Host copy (channels, height, width) float32 of frame `frame`'s tensor."""
+        out = np.empty(self._gp, np.float32)
+        _check(load_library().at_gp_copy(self._h, frame, out.ctypes.data, out.size), "at_gp_copy")
+        return out
 
     # ---- parity taps (apriltag_gpu.h:98-183) -------------------------------
     def _copy(self, stage, frame, nbytes, dtype):

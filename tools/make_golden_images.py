@@ -37,3 +37,8 @@ if __name__ == "__main__":
         rgb = np.asarray(Image.open(path).convert("RGB"))
         Image.fromarray(y_bt601(rgb)).save(DST + name + "_y.png", optimize=True)
         print(name, rgb.shape)
+    # colour input of the game-piece preprocessing row (8(f)4): the 640x640 frame
+    # as decoded, RGB PNG (the tests flip it to the node's bgr8)
+    rgb = np.asarray(Image.open(EXTRA["frc_reefscape_frame6141"]).convert("RGB"))
+    Image.fromarray(rgb).save(DST + "frc_reefscape_frame6141_rgb.png", optimize=True)
+    print("frc_reefscape_frame6141_rgb", rgb.shape)
