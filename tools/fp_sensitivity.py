@@ -79,7 +79,9 @@ def diff(a, b):
 def run():
     import make_golden_vectors as mg
     res = {}
-    for name, W, H, fmt, frame in mg.cases():
+    for name, W, H, fmt, frame, family in mg.cases():
+        if family != "tag36h11":  # the committed study covers the 17 tag36h11 cases
+            continue
         ao.set_fp_perturb(0)
         base = snapshot(W, H, fmt, frame)
         res[name] = {"index_points": int(base["ip"].size), "fitquads": len(base["idx"]),

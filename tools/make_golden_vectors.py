@@ -25,31 +25,39 @@ from ros_vision_amd import synth  # noqa: E402
 def cases():
     codes = dict(ao.family_entries())
     g = os.path.join(ROOT, "tests", "golden")
-    yield "colorimage", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_y.png"))
-    yield "colorimage_notags", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_notags_y.png"))
-    yield "grayimage", 1280, 800, 2, np.asarray(Image.open(g + "/grayimage_y.png"))
-    yield "frc_rebuilt_frame1", 1920, 1080, 2, np.asarray(Image.open(g + "/frc_rebuilt_frame1_y.png"))
-    yield "frc_reefscape_frame6141", 640, 640, 2, np.asarray(Image.open(g + "/frc_reefscape_frame6141_y.png"))
+    T = "tag36h11"
+    yield "colorimage", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_y.png")), T
+    yield "colorimage_notags", 1920, 1080, 2, np.asarray(Image.open(g + "/colorimage_notags_y.png")), T
+    yield "grayimage", 1280, 800, 2, np.asarray(Image.open(g + "/grayimage_y.png")), T
+    yield "frc_rebuilt_frame1", 1920, 1080, 2, np.asarray(Image.open(g + "/frc_rebuilt_frame1_y.png")), T
+    yield "frc_reefscape_frame6141", 640, 640, 2, np.asarray(Image.open(g + "/frc_reefscape_frame6141_y.png")), T
     yield "c1_640x480", 640, 480, 0, synth.to_yuyv(synth.render_board(640, 480, seed=766, ntags=4,
-                                                                       ids=[0, 1, 2, 554], codes=codes)[0])
+                                                                       ids=[0, 1, 2, 554], codes=codes)[0]), T
     for f in (0, 1, 2, 30, 44, 58):  # ids 10f..10f+14 mod 587 across the family
-        yield "c2_720p_f%d" % f, 1280, 720, 0, synth.stream_frame(1280, 720, f, codes=codes)[0]
+        yield "c2_720p_f%d" % f, 1280, 720, 0, synth.stream_frame(1280, 720, f, codes=codes)[0], T
     yield "c4_1080p", 1920, 1080, 0, synth.to_yuyv(synth.render_board(1920, 1080, seed=4242, ntags=24,
-                                                                       codes=codes)[0])
+                                                                       codes=codes)[0]), T
     # more tags than the former 128-detection cap, ids 400.. across the wrap to 0..
     yield "dense_1080p_160tags", 1920, 1080, 0, synth.to_yuyv(synth.render_board(
         1920, 1080, seed=9160, ntags=160, side_range=(50, 64), ids=[(400 + j) % 587 for j in range(160)],
-        codes=codes)[0])
+        codes=codes)[0]), T
     # more accepted quads than the former 512-quad decode queue
-    yield "dots_1080p", 1920, 1080, 2, synth.render_dots(1920, 1080, seed=9512)[0]
+    yield "dots_1080p", 1920, 1080, 2, synth.render_dots(1920, 1080, seed=9512)[0], T
+    # the other classic families (apriltag_utils.cu:13-16): every code of the family on
+    # two 720p boards (tag16h5 also decodes texture quads, as upstream does)
+    for fam, n in (("tag25h9", 35), ("tag16h5", 30)):
+        fc = dict(ao.family_entries(fam))
+        for k, ids in enumerate((list(range(0, 18)), list(range(18, n)))):
+            yield "%s_720p_%d" % (fam, k), 1280, 720, 0, synth.to_yuyv(synth.render_board(
+                1280, 720, seed=7250 + 10 * len(fam) + k, ntags=len(ids), ids=ids, codes=fc, family=fam)[0]), fam
 
 
 def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
 
 
-def run_case(W, H, fmt, frame):
-    o = ao.Oracle(W, H)
+def run_case(W, H, fmt, frame, family="tag36h11"):
+    o = ao.Oracle(W, H, family=family)
     o.detect(frame, fmt)
     pts = o.sorted_points()
     return {
@@ -65,7 +73,7 @@ def run_case(W, H, fmt, frame):
 
 if __name__ == "__main__":
     out = {}
-    for name, W, H, fmt, frame in cases():
-        out[name] = dict(width=W, height=H, fmt=fmt, **run_case(W, H, fmt, frame))
+    for name, W, H, fmt, frame, family in cases():
+        out[name] = dict(width=W, height=H, fmt=fmt, family=family, **run_case(W, H, fmt, frame, family))
         print(name, [d["id"] for d in out[name]["detections"]])
     json.dump(out, open(os.path.join(ROOT, "tests", "golden", "vectors.json"), "w"), indent=1)
