@@ -2594,7 +2594,10 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 
 // Large candidates (size classes 0-2) one per workgroup, then small ones one
 // per wave.
-__global__ __launch_bounds__(256) void k_extents(DevBufs b, Geom g) {
+#ifndef AT_EXT_WAVES
+#define AT_EXT_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVES))) void k_extents(DevBufs b, Geom g) {
   __shared__ int64_t s_red[4][8];
   uint32_t cnt[kNumCls], total = 0, nlarge = 0;
 #pragma unroll
@@ -2676,7 +2679,10 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
 // waves per workgroup, persistent over the small work list.  Everything a blob
 // needs lives in its wave's LDS slice (no global scratch).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_blob_small(DevBufs b, Geom g, Params prm) {
+#ifndef AT_BS_WAVES
+#define AT_BS_WAVES 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_BS_WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<64, kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
@@ -2778,7 +2784,10 @@ struct DecodeShared {
   uint32_t qpre[kMaxBatch + 1];
 };
 
-__global__ __launch_bounds__(kDecodeThreads) void k_decode(DevBufs b, Geom g, Params prm, int B) {
+#ifndef AT_DEC_WAVES
+#define AT_DEC_WAVES 2
+#endif
+__global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(AT_DEC_WAVES))) void k_decode(DevBufs b, Geom g, Params prm, int B) {
   constexpr int RCAP = kMaxRefineSamples;
   __shared__ DecodeShared S;
   const int tid = threadIdx.x;
