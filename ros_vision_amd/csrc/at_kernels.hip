@@ -1418,15 +1418,19 @@ __device__ int homography_wave(const float (*qc)[2], double* A, double* H) {
     }
     __syncthreads();
   }
-  if (lane == 0) {
-    for (int col = 7; col >= 0; col--) {
-      double sum = 0;
-      for (int i = col + 1; i < 8; i++) sum += A[col * 9 + i] * A[i * 9 + 8];
-      A[col * 9 + 8] = (A[col * 9 + 8] - sum) / A[col * 9 + col];
-    }
+  // back substitution, every lane in the serial order with the solution in
+  // registers (the row's A reads are independent LDS broadcasts, issued together)
+  double x[8];
+#pragma unroll
+  for (int col = 7; col >= 0; col--) {
+    double sum = 0;
+#pragma unroll
+    for (int i = col + 1; i < 8; i++) sum += A[col * 9 + i] * x[i];
+    x[col] = (A[col * 9 + 8] - sum) / A[col * 9 + col];
   }
-  __syncthreads();
-  if (lane < 8) H[lane] = A[lane * 9 + 8];
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (lane == k) H[k] = x[k];
   if (lane == 8) H[8] = 1;
   __syncthreads();
   return 0;
@@ -2756,6 +2760,14 @@ __device__ __forceinline__ uint64_t rotate90_n(uint64_t w, int nbits) {
   return w & ((1ull << nbits) - 1);
 }
 constexpr int kMaxTotalWidth = 12;  // total_width of the largest family layout (d <= 8)
+
+// value of lane `l` (uniform) on every lane
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
 // cos / sin of rot * pi/2 as libm returns them (quad_decode's rotation of H)
 __constant__ double c_rot_c[4] = {1.0, 6.123233995736766e-17, -1.0, -1.8369701987210297e-16};
 __constant__ double c_rot_s[4] = {0.0, 1.0, 1.2246467991473532e-16, -1.0};
@@ -2777,8 +2789,7 @@ struct DecodeShared {
   int gmvalid[64];
   double wC[3], bC[3];
   double values[kMaxTotalWidth * kMaxTotalWidth];
-  uint64_t rcode;
-  double margin;
+  uint64_t book[kMaxCodes];  // the family's codebook, loaded once per (persistent) workgroup
   int ok;
   uint32_t item;
   uint32_t qpre[kMaxBatch + 1];
@@ -2814,6 +2825,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
     }
     if (tid == 63) qpre[B] = incl;
   }
+  for (int i = tid; i < prm.fam.ncodes; i += kDecodeThreads) S.book[i] = b.book_code[i];
   __syncthreads();
   const uint32_t nq = qpre[B];
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[128 + k], counts [160 + k])
@@ -2942,15 +2954,30 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       }
       __syncthreads();
       phase(1);
+      // per edge (lane e), the moments in the reference's sample order; samples are
+      // staged 8 at a time in registers so their LDS reads overlap
       if (tid < 4) {
         double Mx = 0, My = 0, Mxx = 0, Mxy = 0, Myy = 0, N = 0;
         const int o = S.samp_off[tid];
-        for (int s = 0; s < S.nsamp[tid] && o + s < RCAP; s++) {
-          const int i = o + s;
-          const double bx = i < kLdsRefine ? S.sx[i] : gsx[i - kLdsRefine];
-          const double by = i < kLdsRefine ? S.sy[i] : gsy[i - kLdsRefine];
-          if (isnan(bx)) continue;
-          Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
+        const int ns = min(S.nsamp[tid], RCAP - o);
+        for (int c = 0; c < ns; c += 8) {
+          double xs[8], ys[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int i = o + c + k;
+            xs[k] = __longlong_as_double(0x7ff8deadbeef0000ll);
+            ys[k] = 0;
+            if (c + k < ns) {
+              xs[k] = i < kLdsRefine ? S.sx[i] : gsx[i - kLdsRefine];
+              ys[k] = i < kLdsRefine ? S.sy[i] : gsy[i - kLdsRefine];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const double bx = xs[k], by = ys[k];
+            if (isnan(bx)) continue;  // (also the padding past the edge's samples)
+            Mx += bx; My += by; Mxx += bx * bx; Mxy += bx * by; Myy += by * by; N++;
+          }
         }
         const double Ex = Mx / N, Ey = My / N;
         const double Cxx = Mxx / N - Ex * Ex, Cxy = Mxy / N - Ex * Ey, Cyy = Myy / N - Ey * Ey;
@@ -3099,30 +3126,33 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       if (t < tw * tw) S.values[t] = S.values[t] + prm.decode_sharpening * shv[r];
     }
     __syncthreads();
-    if (tid == 0) {
+    // code word and scores: lane i reads bit i's value, the scores run in bit
+    // order on every lane (uniform v_readlane loop), the word comes from a ballot
+    double bitv = 0;
+    if (tid < nbits) bitv = S.values[tw * (prm.fam.bity[tid] - minc) + prm.fam.bitx[tid] - minc];
+    const uint64_t white_bits = __ballot(tid < nbits && bitv > 0);  // bit i: data bit i (MSB first in the word)
+    const uint64_t rcode0 = __builtin_bitreverse64(white_bits) >> (64 - nbits);
+    double margin_d;
+    {
       float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
-      uint64_t rcode = 0;
       for (int i = 0; i < nbits; i++) {
-        rcode = rcode << 1;
-        const double v = S.values[tw * (prm.fam.bity[i] - minc) + prm.fam.bitx[i] - minc];
-        if (v > 0) { white_score = (float)(white_score + v); white_cnt++; rcode |= 1; }
+        const double v = readlane_f64(bitv, i);
+        if (v > 0) { white_score = (float)(white_score + v); white_cnt++; }
         else { black_score = (float)(black_score - v); black_cnt++; }
       }
-      S.rcode = rcode;
-      S.margin = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
+      margin_d = fmin((double)(white_score / white_cnt), (double)(black_score / black_cnt));
     }
-    __syncthreads();
     phase(8);
     // quick_decode_codeword: first rotation, then entry, within hamming <= 2
     // (codes are >= 5 apart, so at most one entry matches a rotation)
     uint32_t bc = 0xffffffffu;
     {
       uint64_t r[4];
-      r[0] = S.rcode;
+      r[0] = rcode0;
 #pragma unroll
       for (int k = 1; k < 4; k++) r[k] = rotate90_n(r[k - 1], nbits);
       for (int ent = tid; ent < prm.fam.ncodes; ent += kDecodeThreads) {
-        const uint64_t c = b.book_code[ent];
+        const uint64_t c = S.book[ent];
 #pragma unroll
         for (int rot = 0; rot < 4; rot++) {
           const int hd = __popcll(r[rot] ^ c);
@@ -3133,7 +3163,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
     }
     if (tid == 0) {
-      const float margin = (float)S.margin;
+      const float margin = (float)margin_d;
       if (margin >= 0 && bc != 0xffffffffu) {
         const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
         DevDetection d;
@@ -3238,7 +3268,10 @@ hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint3
 // same pose, splitting only the quartic's root brackets; lane 0 of the quad stores.
 constexpr int kPoseLanes = 4;
 constexpr int kPoseGroupsPerFrame = 8;  // 128 detections per pass, looped beyond
-__global__ __launch_bounds__(64) void k_pose(DevBufs b, Params prm) {
+#ifndef AT_POSE_WAVES
+#define AT_POSE_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AT_POSE_WAVES))) void k_pose(DevBufs b, Params prm) {
   const int f = blockIdx.y;
   const int sub = (int)(threadIdx.x % kPoseLanes);
   // the control block is final once k_decode has finished: block (0, 0) hands it
