@@ -1132,7 +1132,11 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 // (speculatively: reads past the counts stay inside the tile's regions).  Points
 // of later entries (crowded tiles) and of pairs missing from the tile's entries
 // (LDS table overflow in k_boundary) reserve one slot each.
-constexpr int kGrpPre = 4;  // points per thread loaded up front (kBndStage = 1024 per tile)
+// loaded up front, before the tile's counts are known: the first 512 points and
+// 32 entries (typical tiles: ~670 points, ~10 entries), so the speculation reads
+// little past the counts; the rest of a crowded tile follows once they are known
+constexpr int kGrpPre = 2;
+constexpr int kGrpEntPre = 32;
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const int f = blockIdx.y;
   __shared__ uint64_t s_hk[2 * kGrpEnt];
@@ -1146,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const uint32_t n = b.tcnt[tb], ne = b.tent[tb];
   uint64_t ekey = 0;
   uint32_t ebase = kGrpFallback;
-  if (tid < kGrpEnt) {
+  if (tid < kGrpEntPre) {
     ekey = b.pent_key[tb * kLdsPairSlots + tid];
     ebase = b.pent_cnt[tb * kLdsPairSlots + tid];
   }
@@ -1154,6 +1158,10 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
 #pragma unroll
   for (int k = 0; k < kGrpPre; k++) pv[k] = pts[tid + 256 * k];
   if (st & (kStatusPairsOverflow | kStatusHashFull)) return;
+  if (tid >= kGrpEntPre && tid < kGrpEnt && (uint32_t)tid < ne) {
+    ekey = b.pent_key[tb * kLdsPairSlots + tid];
+    ebase = b.pent_cnt[tb * kLdsPairSlots + tid];
+  }
   const uint64_t* ht_key = b.ht_key + (size_t)f * kHashSlots;
   const uint32_t* ht_off = b.ht_off + (size_t)f * kHashSlots;
   const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
