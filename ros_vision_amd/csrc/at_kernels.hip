@@ -1587,6 +1587,7 @@ struct BlobShared {
   uint64_t keys[kKeySlots<NT, CAP>];
   uint32_t bcnt[kKeySlots<NT, CAP> / 4];  // theta bucket counts, two u16 per word (team_bucket_sort)
   uint64_t pks[16];                        // the top-10 peak keys (peaks themselves stay in registers)
+  uint64_t wtop[NT > 64 ? NT / 64 * 10 : 1];  // each wave's top-10 peak keys (teams of more than one wave)
   // inclusive prefix moments at the indices FitQuads reads: [k] = P[pi[k]],
   // [10 + k] = P[pi[k] - 1], [20] = P[n - 1]
   uint32_t tMx[21], tMy[21], tW[21];
@@ -2180,15 +2181,25 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   // error in cub's float radix order, then point index).  Each thread keeps its
   // chunk's peaks in registers: strict maxima are never adjacent, so chunk
   // position k has slot k / 2 to itself
-  auto filt_at = [&](uint32_t t) -> double {
+  // the chunk's error window errv[t0 - 4 .. t0 + kC + 3] (cyclic) staged in
+  // registers, every LDS read issued at once; filt(k) = filtered error of point
+  // t0 + k, k = -1 .. c, summed in the reference's tap order
+  constexpr int kEW = kC + 8;
+  float ew[kEW];
+  if (t0 < t1) {
+#pragma unroll
+    for (int j = 0; j < kEW; j++) {
+      uint32_t idx = t0 + 2 * n + j - 4;
+      idx -= idx >= n ? n : 0;
+      idx -= idx >= n ? n : 0;
+      idx -= idx >= n ? n : 0;
+      ew[j] = errv[idx];
+    }
+  }
+  auto filt_k = [&](int k) -> double {  // k + 1 + j indexes ew: constant after unrolling
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < 7; j++) {
-      uint32_t idx = t + n + j - 3;
-      idx -= idx >= n ? n : 0;
-      idx -= idx >= n ? n : 0;
-      acc += (double)errv[idx] * (double)c_filter[j];
-    }
+    for (int j = 0; j < 7; j++) acc += (double)ew[k + 1 + j] * (double)c_filter[j];
     return acc;
   };
   constexpr int kPR = (kC + 1) / 2;
@@ -2197,12 +2208,12 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   for (int j = 0; j < kPR; j++) mine[j] = ~0ull;
   uint32_t nmine = 0;
   if (t0 < t1) {
-    double fprev = filt_at(t0 == 0 ? n - 1 : t0 - 1), fcur = filt_at(t0);
+    double fprev = filt_k(-1), fcur = filt_k(0);
 #pragma unroll
     for (int k = 0; k < kC; k++) {
       const uint32_t t = t0 + k;
       if (k >= (int)c || t >= t1) break;
-      const double fnext = filt_at(t + 1 == n ? 0 : t + 1);
+      const double fnext = filt_k(k + 1);
       if (fcur > fprev && fcur > fnext) {
         const float ef = (float)(-fcur);
         uint32_t u = __float_as_uint(ef);
@@ -2222,18 +2233,50 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     // over the keys (unique: the point index is in the low word) above the
     // previous pick -- instead of sorting every peak
     const int ntop = npk < (uint32_t)kNMaxima ? (int)npk : kNMaxima;
-    uint64_t* red = reinterpret_cast<uint64_t*>(S.red_f64);
     uint64_t last = 0;
-    for (int r = 0; r < ntop; r++) {
-      uint64_t m = ~0ull;
+    if constexpr (NT == 64) {
+      for (int r = 0; r < ntop; r++) {
+        uint64_t m = ~0ull;
 #pragma unroll
-      for (int j = 0; j < kPR; j++) {
-        const uint64_t k = mine[j];
-        if ((r == 0 || k > last) && k < m) m = k;
+        for (int j = 0; j < kPR; j++) {
+          const uint64_t k = mine[j];
+          if ((r == 0 || k > last) && k < m) m = k;
+        }
+        m = wave_reduce(m, MinOp());
+        if (tid == 0) pks[r] = m;
+        last = m;
       }
-      m = team_reduce<NT>(m, MinOp(), red);
-      if (tid == 0) pks[r] = m;
-      last = m;
+    } else {
+      // every wave selects its own top ntop (wave minima, no barriers), then wave 0
+      // the top ntop of those candidates: the team's top ntop is among them
+      const int w = tid >> 6, ln = tid & 63;
+      for (int r = 0; r < ntop; r++) {
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int j = 0; j < kPR; j++) {
+          const uint64_t k = mine[j];
+          if ((r == 0 || k > last) && k < m) m = k;
+        }
+        m = wave_reduce(m, MinOp());
+        if (ln == 0) S.wtop[w * kNMaxima + r] = m;
+        last = m;
+      }
+      team_sync<NT>();
+      if (w == 0) {
+        constexpr int NC = NT / 64 * kNMaxima;  // <= 80 candidates, two per lane
+        uint64_t c0 = ~0ull, c1 = ~0ull;
+        if (ln < NC && (ln % kNMaxima) < ntop) c0 = S.wtop[ln];
+        if (ln + 64 < NC && ((ln + 64) % kNMaxima) < ntop) c1 = S.wtop[ln + 64];
+        last = 0;
+        for (int r = 0; r < ntop; r++) {
+          uint64_t m = ~0ull;
+          if ((r == 0 || c0 > last) && c0 < m) m = c0;
+          if ((r == 0 || c1 > last) && c1 < m) m = c1;
+          m = wave_reduce(m, MinOp());
+          if (ln == 0) pks[r] = m;
+          last = m;
+        }
+      }
     }
     team_sync<NT>();
   }
