@@ -717,6 +717,10 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
   }
 }
 
+// KEPT (throughput mode): the size test comes with the root word (k_ccl_keep);
+// latency mode skips that kernel and reads the size plane (one more round trip
+// here, one launch less on the chain)
+template <bool KEPT>
 __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
@@ -778,7 +782,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     if (e < kTN) {
-      const bool kept = lv[k] != 0xffffffffu && (lv[k] & kKeptBit);
+      const bool kept = lv[k] != 0xffffffffu && (KEPT ? (lv[k] & kKeptBit) != 0 : b.size[fo + lv[k]] >= 25);
       s_tlab[e] = lv[k] & ~kKeptBit;
       s_tthr[e] = kept ? tv[k] : (uint8_t)127;
     }
@@ -1018,16 +1022,26 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   stamp(2);
   if (n <= 1024) {
     // rank sort (keys are unique: the slot rides in the low bits); t_key is free
-    // once the lookup table has been written out above
-    const uint64_t key = tid < (int)n ? s_list[tid] : 0;
-    uint32_t r = 0;
-    if (tid < (int)n) {
-      int j = 0;
-      for (; j + 4 <= (int)n; j += 4)
+    // once the lookup table has been written out above.  P = 1024 / n threads per
+    // key, each counting the smaller keys of a 1/P slice of the list (a frame's
+    // ~400 pairs: 2 threads per key, half the serial LDS reads)
+    const int P = (int)(1024 / (n ? n : 1u));
+    uint32_t* s_rank = reinterpret_cast<uint32_t*>(t_key + 2048);
+    if (tid < (int)n) s_rank[tid] = 0;
+    __syncthreads();
+    if (tid < P * (int)n) {
+      const int i = tid % (int)n, h = tid / (int)n;
+      const uint64_t key = s_list[i];
+      const int j1 = (int)(((uint32_t)h + 1) * n / (uint32_t)P);
+      int j = (int)((uint32_t)h * n / (uint32_t)P);
+      uint32_t r = 0;
+      for (; j + 4 <= j1; j += 4)
         r += (s_list[j] < key) + (s_list[j + 1] < key) + (s_list[j + 2] < key) + (s_list[j + 3] < key);
-      for (; j < (int)n; j++) r += s_list[j] < key;
-      t_key[r] = key;
+      for (; j < j1; j++) r += s_list[j] < key;
+      if (r) atomicAdd(&s_rank[i], r);
     }
+    __syncthreads();
+    if (tid < (int)n) t_key[s_rank[tid]] = s_list[tid];
     __syncthreads();
     if (tid < (int)n) s_list[tid] = t_key[tid];
     __syncthreads();
@@ -3496,14 +3510,16 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(3, st, 0);
   if (on(3)) {
     hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
-    hipLaunchKernelGGL(k_ccl_keep, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+    if (g.ctw != 32) hipLaunchKernelGGL(k_ccl_keep, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
   }
   tk(3, st, 1);
   mark();
   {
     dim3 blk(64, 4), grd(g.BTX, g.BTY, B);
     tk(4, st, 0);
-    if (on(4)) hipLaunchKernelGGL(k_boundary, grd, blk, 0, st, b, g);
+    if (!on(4)) {}
+    else if (g.ctw != 32) hipLaunchKernelGGL(k_boundary<true>, grd, blk, 0, st, b, g);
+    else hipLaunchKernelGGL(k_boundary<false>, grd, blk, 0, st, b, g);
     tk(4, st, 1);
     mark();
   }
