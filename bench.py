@@ -57,6 +57,9 @@ def parse():
                          "detector stream so the batches in flight run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
+    ap.add_argument("--timed-kernel", default=None,
+                    help="kernel timed live for the roofline (default: the dominant one of the stage profile; "
+                         "lets a traced run without the stage-profile pass time the same kernel)")
     ap.add_argument("--no-kernel-timer", action="store_true",
                     help="no HIP events around the dominant kernel (graph replay in the timed region)")
     ap.add_argument("--ingest", choices=["local", "scatter"], default="local",
@@ -292,7 +295,7 @@ def main():
             prof.collect()
         stages, stage_batches = prof.stage_times()
         prof.set_profiling(False)
-    dominant = max(stages, key=stages.get) if stages else "k_blob"
+    dominant = args.timed_kernel or (max(stages, key=stages.get) if stages else "k_blob")
     # live per-launch time of the dominant kernel inside the timed region
     ktimer = None if args.no_kernel_timer else dominant
     for d in dets:

@@ -17,7 +17,7 @@ export TMPDIR=/tmp
 SHORT="$ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 4 --warmup 1 --latency-frames 0"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
-  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 40 --warmup 3 --latency-frames 0 \
+  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --timed-kernel ${TIMED:-k_blob_small} --batch $BATCH --steps 40 --warmup 3 --latency-frames 0 \
   > "$OUT/trace_timed_bench.json" 2> "$OUT/trace_timed.err"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $SHORT \
   > /dev/null 2> "$OUT/pmc_fetch.err"
