@@ -1820,17 +1820,11 @@ constexpr uint32_t kRegSortMaxBucket = 512;
 // are theta >> s (nb = 2^m buckets of width 2^(26-m); theta < 2^26).  Returns
 // false with the keys in S.keys in load order when a bucket exceeds 32 keys.
 template <int CAP>
-__device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, int n) {
+__device__ bool wave_bucket_sort_kv(BlobShared<64, CAP>& S, uint64_t (&kv)[CAP / 64], int n) {
   static_assert(CAP % 64 == 0 && CAP <= 512, "wave sort: at most 8 keys per lane");
   static_assert(kThetaSpan <= (1ull << 26), "theta fits 26 bits");
   constexpr int KPL = CAP / 64;
   const uint32_t lane = lane_id();
-  uint64_t kv[KPL];
-#pragma unroll
-  for (int j = 0; j < KPL; j++) {
-    const int t = j * 64 + (int)lane;
-    kv[j] = t < n ? grp[t] : ~0ull;
-  }
   int nb = 32;
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n, power of two, <= 256
   const int sh = 26 - __builtin_ctz((unsigned)nb);
@@ -1918,6 +1912,20 @@ __device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, in
     if (j * 64 + (int)lane < n) S.keys[rk[j]] = kv[j];
   team_sync<64>();
   return true;
+}
+
+// keys (theta, plane, y, x) from global memory: slot t = j * 64 + lane
+template <int CAP>
+__device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, int n) {
+  constexpr int KPL = CAP / 64;
+  const uint32_t lane = lane_id();
+  uint64_t kv[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    const int t = j * 64 + (int)lane;
+    kv[j] = t < n ? grp[t] : ~0ull;
+  }
+  return wave_bucket_sort_kv<CAP>(S, kv, n);
 }
 
 // Workgroup-team variant of wave_bucket_sort for the blobs whose keys do not
@@ -2043,6 +2051,92 @@ __device__ __forceinline__ Mom6 prefix_at(const BlobShared<NT, CAP>& S, const ui
   return p;
 }
 
+// Latency mode: k_extents' work for one small candidate (<= kSmallBlob points)
+// inside the small-blob wave itself: MinMaxExtents (P3), SelectBlobs (P4) and the
+// (theta, plane, y, x) keys with the line-fit weight (P5, TransformLineFitPoint),
+// the same expressions as extents_item, but the keys stay in registers (slot
+// t = j * 64 + lane) for the sort: no key store and reload through HBM, no
+// separate launch: 6 us less on the B = 1 chain.  (Throughput mode keeps
+// k_extents: the fused item's extra dependent round trip, with four waves per
+// SIMD, costs more there than the key store and reload.)  Returns SelectBlobs'
+// decision (uniform across the wave).
+__device__ bool small_extents_keys(const DevBufs& b, const Geom& g, int f, uint32_t rank, uint32_t n,
+                                   const uint64_t* grp, uint64_t (&kv)[kSmallBlob / 64]) {
+  constexpr int U = kSmallBlob / 64;
+  const int lane = (int)lane_id();
+  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t t = (uint32_t)(u * 64 + lane);
+    kv[u] = t < n ? grp[t] : 0;
+  }
+  uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
+  int32_t sgx = 0, sgy = 0;
+  int64_t spg = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if ((uint32_t)(u * 64 + lane) >= n) continue;
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
+    const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
+    const bool b2w = (k & 8) != 0;
+    const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
+    mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
+    sgx += gx; sgy += gy;
+    spg += (int64_t)px * gx + (int64_t)py * gy;
+  }
+  Ext e;
+  e.min_x = wave_reduce(mnx, MinOp()); e.max_x = wave_reduce(mxx, MaxOp());
+  e.min_y = wave_reduce(mny, MinOp()); e.max_y = wave_reduce(mxy, MaxOp());
+  e.gx_sum = wave_reduce(sgx, AddOp()); e.gy_sum = wave_reduce(sgy, AddOp());
+  e.pg_sum = wave_reduce(spg, AddOp());
+  e.count = n;
+  bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
+  keep = keep && !((double)ext_dot(e) < 0.0);
+  if (!keep) return false;
+  if (lane == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;  // (parity taps, host statistics)
+  const double cx = ext_cx(e), cy = ext_cy(e);
+  uint32_t gp[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const int32_t ix = (int32_t)(((k >> 14) & 0x3ff) * 2 + dx_of(dxy) + 1) / 2;
+    const int32_t iy = (int32_t)(((k >> 4) & 0x3ff) * 2 + dy_of(dxy) + 1) / 2;
+    const bool in = (uint32_t)(u * 64 + lane) < n && ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd;
+    const int32_t at = in ? iy * g.Wd + ix : g.Wd + 1;
+    gp[u] = (uint32_t)dec[at - 1] | ((uint32_t)dec[at + 1] << 8) | ((uint32_t)dec[at - g.Wd] << 16) |
+            ((uint32_t)dec[at + g.Wd] << 24);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if ((uint32_t)(u * 64 + lane) >= n) {
+      kv[u] = ~0ull;
+      continue;
+    }
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
+    const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
+    const float dyf = (float)((double)py - cy);
+    const float dxf = (float)((double)px - cx);
+    const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
+    long long ti = (long long)rintf(theta);
+    if (ti < 0) ti = 0;
+    const int32_t ix = (int32_t)(px + 1) / 2, iy = (int32_t)(py + 1) / 2;
+    int32_t Wt = 1;
+    if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
+      const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
+      const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
+      Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+    }
+    kv[u] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
+            ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
+  }
+  return true;
+}
+
 // Processes one work item (frame, pair rank) with a team of NT threads.
 // gpk: this team's global overflow area for peak keys beyond kPeakCap (large
 // blobs only; nullptr when the LDS area always suffices).
@@ -2057,7 +2151,7 @@ __device__ __forceinline__ PairInfo load_pair_info(const DevBufs& b, uint32_t w)
   return PairInfo{b.pair_cnt[i], b.pair_off[i], b.pair_sel[i]};
 }
 
-template <int NT, int CAP>
+template <int NT, int CAP, bool FUSE = false>
 __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S, uint64_t* gpk,
                           const uint32_t* combo, uint32_t w, PairInfo pi_, uint32_t* pacc) {
   constexpr int kC = (CAP + NT - 1) / NT;  // max points per thread chunk
@@ -2088,13 +2182,29 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   big = n > 2048;
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts + pi_.off;
 
-  // extents, SelectBlobs and the theta keys come from k_extents
-  if (pi_.sel == 0) return;  // uniform across the team
-
-  if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
-  const uint32_t bi = rank & 0xfff;
-  phase(0);
+  // extents, SelectBlobs and the theta keys: from k_extents, or here (FUSE)
   bool sorted = false, in_lds = false;
+  const uint32_t bi = rank & 0xfff;
+  if constexpr (NT == 64 && FUSE) {
+    uint64_t kv[kSmallBlob / 64];
+    if (!small_extents_keys(b, g, f, rank, n, grp, kv)) return;  // uniform across the wave
+    if (tid == 0) pacc[20] += n;
+    phase(0);
+    phase(1);
+    if (n >= 64) {
+      sorted = wave_bucket_sort_kv<CAP>(S, kv, (int)n);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSmallBlob / 64; j++)
+        if (j * 64 + (int)lane < (int)n) S.keys[j * 64 + lane] = kv[j];
+      team_sync<NT>();
+      sorted = team_bucket_sort<NT, CAP>(S, (int)n);
+    }
+    in_lds = true;
+  } else {
+  if (pi_.sel == 0) return;  // uniform across the team
+  if (tid == 0) pacc[20] += n;  // points of kept blobs this team processed (batch statistics)
+  phase(0);
   if constexpr (NT == 64) {
     if (n >= 64) {  // keys go straight from global memory into registers
       phase(1);
@@ -2113,6 +2223,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     phase(1);
     team_sync<NT>();
     sorted = team_bucket_sort<NT, CAP>(S, (int)n);
+  }
   }
   if (!sorted) {
     int np2 = 64;
@@ -2680,6 +2791,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVE
     work_item(b, cnt, 0, kNumCls, it, &w);
     extents_item<256>(b, g, w, s_red);
   }
+  if (g.ctw == 32) return;  // latency mode: k_blob_small<true> does the small candidates itself
   const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   for (uint32_t it = nlarge + gw; it < total; it += nw) {
     uint32_t w = 0;
@@ -2751,7 +2863,8 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
 #ifndef AT_BS_WAVES
 #define AT_BS_WAVES 4
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_BS_WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm) {
+template <bool FUSE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : AT_BS_WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<64, kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
@@ -2784,7 +2897,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_BS_WAVES
     const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
     uint32_t w2 = 0;
     if (item + 2 * nwaves < nwork) work_item(b, s_cnt, kNumLargeCls, kNumCls, item + 2 * nwaves, &w2);
-    blob_item<64, kSmallBlob>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
+    blob_item<64, kSmallBlob, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
     w = w1;
     pi = pi1;
     w1 = w2;
@@ -3551,7 +3664,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   };
   auto blob_small = [&](hipStream_t s) {
     tk(8, s, 0);
-    if (on(8)) hipLaunchKernelGGL(k_blob_small, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    if (!on(8)) {}
+    else if (g.ctw == 32) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    else hipLaunchKernelGGL(k_blob_small<false>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
     tk(8, s, 1);
   };
   if (ev || !st2) {

@@ -85,6 +85,22 @@ def test_batch_matches_single(gpu, oracle_mod):
         assert compare_detections(batch[c], orc.detections()) == []
 
 
+def test_throughput_mode_matches_oracle(gpu, oracle_mod):
+    """max_batch >= 8 selects the throughput-mode kernels (64-wide CCL tiles,
+    k_ccl_keep + k_boundary<true>, k_extents for every candidate, k_blob_small
+    without fused extents, 256-thread large-blob teams): per-frame stages and
+    detections identical to the oracle, as in latency mode."""
+    from ros_vision_amd import synth
+    frames = [synth.stream_frame(1280, 720, f)[0] for f in (3, 17, 31, 45, 58, 5, 9, 12)]
+    det = gpu.GpuDetector(1280, 720, max_batch=8)
+    batch = det.detect_batch(frames)
+    for c, f in enumerate(frames):
+        orc = oracle_mod.Oracle(1280, 720)
+        orc.detect(f, 0)
+        assert compare_frame(det, orc, frame_idx=c) == []
+        assert compare_detections(batch[c], orc.detections()) == []
+
+
 def test_1080p_parity(gpu, oracle_mod):
     """Config C4 geometry (1920x1080, 24 tags)."""
     from ros_vision_amd import synth
