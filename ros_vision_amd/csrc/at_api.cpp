@@ -300,7 +300,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
   p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
   p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
-  p.taps = !(getenv("AT_NO_TAPS") && atoi(getenv("AT_NO_TAPS")));
+  p.taps = 0;  // debug taps off: at_set_debug_taps
   p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
   p.pipe_stop = getenv("AT_DIAG_PIPE_STOP") ? atoi(getenv("AT_DIAG_PIPE_STOP")) : 0;
   p.fam = family_desc(*fam);
@@ -906,6 +906,17 @@ int at_gp_preprocess_device(const uint8_t* bgr, int width, int height, float* ou
              : AT_E_HIP;
 }
 
+int at_set_debug_taps(at_detector* d, int enable) {
+  if (!d) return AT_E_INVALID;
+  if (hipSetDevice(d->device) != hipSuccess) return AT_E_HIP;
+  if (d->pending && hipEventSynchronize(d->ev_done) != hipSuccess) return AT_E_HIP;
+  if (d->prm.taps != (enable ? 1 : 0)) {
+    d->prm.taps = enable ? 1 : 0;
+    drop_graphs(d);  // the captured sequences carry the old parameters
+  }
+  return AT_OK;
+}
+
 int at_frame_status(at_detector* d, int frame) {
   if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
   const uint32_t s = d->h_ctrl[kCtlStatus * d->B + frame];
@@ -1012,7 +1023,9 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       return (long long)(np * 8);
     }
     case AT_STAGE_BLOB_POINTS: {
-      // IndexPoint keys of the selected pairs, in rank order
+      // IndexPoint keys of the selected pairs, in rank order (written by the blob
+      // kernels only while the debug taps are on)
+      if (!d->prm.taps) return AT_E_INVALID;
       const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[kCtlNpairs * B + frame], (uint32_t)kMaxPairs);
       std::vector<uint32_t> cnt(npairs), off(npairs), sel(npairs);
       if (npairs) {

@@ -32,7 +32,7 @@ EXPORTS = [
     "at_strerror", "at_family_num_known", "at_family_entry", "at_abi_version",
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
-    "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device",
+    "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -177,6 +177,8 @@ def load_library(path: str = LIB_PATH):
     L.at_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     L.at_tag_detections.argtypes = [C.POINTER(AtPose), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                     C.POINTER(AtTagDetection)]
+    if hasattr(L, "at_set_debug_taps"):
+        L.at_set_debug_taps.argtypes = [C.c_void_p, C.c_int]
     if hasattr(L, "at_gp_enable"):  # (A/B builds of older sources lack it)
         L.at_gp_enable.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
         L.at_gp_tensor.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
@@ -242,10 +244,11 @@ class GpuDetector:
     """Drop-in for frc971::apriltag::GpuDetector on MI355X (one instance per camera)."""
 
     MAX_DETECTIONS = 1024  # per frame returned to Python (the library keeps up to 4096 per frame)
+    DEBUG_TAPS = False     # default of debug_taps (the parity tests turn it on for their module)
 
     def __init__(self, width, height, camera_matrix: CameraMatrix = TEST_CAMERA,
                  distortion_coefficients: DistCoeffs = TEST_DIST, family="tag36h11",
-                 max_batch=1, device=0, pinned_out=False, **overrides):
+                 max_batch=1, device=0, pinned_out=False, debug_taps=None, **overrides):
         L = load_library()
         self.width, self.height, self.max_batch = int(width), int(height), int(max_batch)
         cfg = AtConfig()
@@ -263,6 +266,8 @@ class GpuDetector:
         h = C.c_void_p()
         _check(L.at_create(C.byref(cfg), C.byref(cam), C.byref(h)), "at_create")
         self._h = h
+        if self.DEBUG_TAPS if debug_taps is None else debug_taps:
+            _check(L.at_set_debug_taps(h, 1), "at_set_debug_taps")  # copy_blob_points needs them
         self._cap = self.MAX_DETECTIONS
         self._out_t = None
         if pinned_out:

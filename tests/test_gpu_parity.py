@@ -15,7 +15,9 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def gpu():
     import ros_vision_amd as rva
-    return rva
+    rva.GpuDetector.DEBUG_TAPS = True  # the IndexPoint tap (copy_blob_points) for every detector here
+    yield rva
+    rva.GpuDetector.DEBUG_TAPS = False
 
 
 def _real(golden_dir, name):

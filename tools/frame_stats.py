@@ -12,7 +12,7 @@ from ros_vision_amd import synth
 
 W, H, N = 1280, 720, 8
 codes = dict(rva.family_entries())
-det = rva.GpuDetector(W, H)
+det = rva.GpuDetector(W, H, debug_taps=True)
 for i in range(N):
     gray, _ = synth.render_board(W, H, seed=766000 + i, ntags=15, codes=codes)
     det.detect(synth.to_yuyv(gray))

@@ -12,7 +12,7 @@ out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 os.makedirs(out, exist_ok=True)
 cases = [("syn1080", 1920, 1080, synth.to_yuyv(synth.render_board(1920, 1080, seed=4242, ntags=24)[0]), 0)]
 for name, W, H, frame, fmt in cases:
-    det = rva.GpuDetector(W, H)
+    det = rva.GpuDetector(W, H, debug_taps=True)
     dets = det.detect(frame, fmt)
     np.savez_compressed(os.path.join(out, "dump_%s.npz" % name),
                         blob_points=det.copy_blob_points(), points=det.copy_points(),
