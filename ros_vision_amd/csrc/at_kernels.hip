@@ -3007,7 +3007,9 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
   __syncthreads();
   const uint32_t nq = qpre[B];
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[128 + k], counts [160 + k])
-  uint32_t pacc[21] = {0};
+  // (in LDS rather than 21 registers per lane)
+  __shared__ uint32_t pacc[21];
+  if (tid < 21) pacc[tid] = 0;
   uint64_t t_last = 0;
   auto phase = [&](int k) {
     if (prm.probe && tid == 0) {
@@ -3340,28 +3342,28 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
     }
-    if (tid == 0) {
-      const float margin = (float)margin_d;
-      if (margin >= 0 && bc != 0xffffffffu) {
-        const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
-        DevDetection d;
-        d.id = b.book_id[ent];
-        d.hamming = hd;
-        d.decision_margin = margin;
-        d.blob_rank = (int32_t)qrank;
-        const double R[9] = {c_rot_c[rot], -c_rot_s[rot], 0, c_rot_s[rot], c_rot_c[rot], 0, 0, 0, 1};
-        for (int i = 0; i < 3; i++)
-          for (int j = 0; j < 3; j++) {
-            double acc = 0;
-            for (int k = 0; k < 3; k++) acc += S.H[i * 3 + k] * R[k * 3 + j];
-            d.H[i * 3 + j] = acc;
-          }
-        hproject(d.H, 0, 0, &d.c[0], &d.c[1]);
-        for (int i = 0; i < 4; i++) {
-          const int tcx = (i == 1 || i == 2) ? 1 : -1;
-          const int tcy = (i < 2) ? 1 : -1;
-          hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
+    const float margin = (float)margin_d;
+    if (margin >= 0 && bc != 0xffffffffu) {  // uniform (bc is the wave minimum)
+      const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
+      DevDetection d;
+      d.id = b.book_id[ent];
+      d.hamming = hd;
+      d.decision_margin = margin;
+      d.blob_rank = (int32_t)qrank;
+      const double R[9] = {c_rot_c[rot], -c_rot_s[rot], 0, c_rot_s[rot], c_rot_c[rot], 0, 0, 0, 1};
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          double acc = 0;
+          for (int k = 0; k < 3; k++) acc += S.H[i * 3 + k] * R[k * 3 + j];
+          d.H[i * 3 + j] = acc;
         }
+      hproject(d.H, 0, 0, &d.c[0], &d.c[1]);
+      for (int i = 0; i < 4; i++) {
+        const int tcx = (i == 1 || i == 2) ? 1 : -1;
+        const int tcy = (i < 2) ? 1 : -1;
+        hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
+      }
+      if (tid == 0) {
         const uint32_t di = atomicAdd(b.ndets + f, 1u);
         if (di < (uint32_t)kMaxDets) {
           b.dets[(size_t)f * kMaxDets + di] = d;
@@ -3449,6 +3451,10 @@ constexpr int kPoseGroupsPerFrame = 8;  // 128 detections per pass, looped beyon
 #ifndef AT_POSE_WAVES
 #define AT_POSE_WAVES 1
 #endif
+// WAVE (latency mode): a whole wave per detection (the quartic's root brackets
+// searched by lane groups, solve_poly_level_wave); else four lanes (a DPP quad)
+// per detection, one bracket each.
+template <bool WAVE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AT_POSE_WAVES))) void k_pose(DevBufs b, Params prm) {
   const int f = blockIdx.y;
   const int sub = (int)(threadIdx.x % kPoseLanes);
@@ -3457,13 +3463,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AT_POSE_WAVE
   if (blockIdx.x == 0 && blockIdx.y == 0)
     for (uint32_t w = threadIdx.x; w < b.ctrl_words; w += 64) b.hctrl[w] = b.ctrl[w];
   const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
-  for (uint32_t i = blockIdx.x * (64 / kPoseLanes) + threadIdx.x / kPoseLanes; i < n;  // uniform across the quad
-       i += gridDim.x * (64 / kPoseLanes)) {
+  constexpr uint32_t kPer = WAVE ? 1 : 64 / kPoseLanes;  // detections per wave
+  for (uint32_t i = blockIdx.x * kPer + (WAVE ? 0 : threadIdx.x / kPoseLanes); i < n;  // uniform across the quad
+       i += gridDim.x * kPer) {
     DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
     double R[9], t[3], err[2];
-    pose::estimate_tag_pose(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
-                            (prm.probe && f == 0 && i == 0 && sub == 0) ? b.probe + 16 : nullptr);
-    if (sub == 0) {
+    pose::estimate_tag_pose<WAVE>(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
+                                  (prm.probe && f == 0 && i == 0 && threadIdx.x == 0) ? b.probe + 16 : nullptr);
+    if (WAVE ? threadIdx.x == 0 : sub == 0) {
       DevDetection& h = b.hdets[(size_t)f * kMaxDets + i];
 #pragma unroll
       for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
@@ -3693,8 +3700,11 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(10, st, 1);
   mark();
   tk(11, st, 0);
-  if (prm.tag_size > 0 && on(11))
-    hipLaunchKernelGGL(k_pose, dim3(kPoseGroupsPerFrame, B), dim3(64), 0, st, b, prm);
+  // latency mode: a wave per detection; throughput mode: four lanes per detection
+  if (prm.tag_size > 0 && on(11)) {
+    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_pose<true>, dim3(32, B), dim3(64), 0, st, b, prm);
+    else hipLaunchKernelGGL(k_pose<false>, dim3(kPoseGroupsPerFrame, B), dim3(64), 0, st, b, prm);
+  }
   tk(11, st, 1);
   mark();
   if (split_err != hipSuccess) return split_err;

@@ -193,10 +193,13 @@ __device__ __forceinline__ M3 calculate_F(const V3& v) {
 // then R <- polar(M3).  As upstream, the returned t belongs to the R before the last step
 // and the error to the final (R, t).
 __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, int n_steps, int* steps = nullptr) {
+  M3 Gx, Gy, Fs, Fxy;
+  {
+  // (F_j is recomputed for the error below instead of being held across the loop:
+  // 72 registers fewer while the iteration runs)
   M3 F[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) F[k] = calculate_F(v[k]);
-  M3 Gx, Gy, Fs, Fxy;
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
@@ -214,6 +217,7 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
       Fs.m[i][j] = fs;
       Fxy.m[i][j] = fxy;
     }
+  }
   M3 ImA;
 #pragma unroll
   for (int i = 0; i < 3; i++)
@@ -282,8 +286,9 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
   double error = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
+    const M3 Fj = calculate_F(v[j]);
     const V3 x = v_add(mv(*R, p[j]), *t);
-    const V3 e = v_sub(x, mv(F[j], x));  // (I - F) x
+    const V3 e = v_sub(x, mv(Fj, x));  // (I - F) x
     error += v_dot(e, e);
   }
   return error;
@@ -389,6 +394,109 @@ __device__ int solve_poly_level(const double* p, int degree, const double* der_r
   return n;
 }
 
+// The same level with a whole wave per detection (latency mode, k_decode<true>):
+// bracket s (<= n_der <= 3) belongs to lanes 16 s .. 16 s + 15, which search it in
+// parallel -- each round every lane evaluates the polynomial at one of 16 interior
+// points of (lower, upper) and the group keeps the sub-interval where the sign
+// changes (a ballot), shrinking the bracket 17-fold per round, until no interior
+// point is representable.  The end points and the sign test are upstream's; the root
+// is the converged bracket end on the f <= 0 side (upstream's safeguarded Newton
+// converges to the same double to within an ulp or two; orthogonal iteration then
+// contracts any such difference).  No divisions, ~20 rounds instead of a
+// data-dependent Newton/bisection loop.
+__device__ __forceinline__ double horner(const double* p, int degree, double x) {
+  double r = p[degree];
+  for (int i = degree - 1; i >= 0; i--) r = fma(r, x, p[i]);
+  return r;
+}
+// This lane's bracket root (my_has: one exists); the caller gathers.
+__device__ void solve_poly_level_wave_lane(const double* p, int degree, const double* der_roots, int n_der,
+                                           double& my_root, int& my_has) {
+  double MAX_ROOT = 1000;
+  if (p[degree] != 0) {
+    double cb = 0;
+    const double rl = 1.0 / fabs(p[degree]);  // (the bound only has to exceed every root)
+    for (int i = 0; i < degree; i++) cb = fmax(cb, fabs(p[i]) * rl);
+    MAX_ROOT = fmin(MAX_ROOT, 1 + cb * (1 + 0x1p-40));
+  }
+  const int lane = (int)__lane_id();
+  const int sub = lane >> 4, j = lane & 15;
+  my_root = 0;
+  my_has = 0;
+  if (sub <= n_der) {
+    const double mn = sub == 0 ? -MAX_ROOT : der_roots[sub - 1];
+    const double mx = sub == n_der ? MAX_ROOT : der_roots[sub];
+    const double fmn = polyval(p, degree, mn), fmx = polyval(p, degree, mx);
+    if (fmn * fmx < 0) {
+      double lower = fmn < fmx ? mn : mx, upper = fmn < fmx ? mx : mn;
+      if (degree == 2 && p[2] != 0) {
+        // a quadratic's bracketed root in closed form (the cancellation-free pair
+        // q / a, c / q); the search below only if rounding put it outside the bracket
+        const double disc = p[1] * p[1] - 4 * p[2] * p[0];
+        if (disc >= 0) {
+          const double q = -0.5 * (p[1] + copysign(sqrt(disc), p[1]));
+          const double ra = q / p[2], rb = q != 0 ? p[0] / q : ra;
+          const double lo = fmin(mn, mx), hi = fmax(mn, mx);
+          const bool ina = ra >= lo && ra <= hi, inb = rb >= lo && rb <= hi;
+          if (ina != inb) {
+            lower = upper = ina ? ra : rb;
+          }
+        }
+      }
+      // down to 2^-30 of max(1, |root|), then two Newton steps kept inside the
+      // final bracket (quadratic convergence: far below what orthogonal iteration
+      // resolves; upstream's Newton stops at the same double within an ulp or two)
+      for (int it = 0; it < 24 && fabs(upper - lower) > 0x1p-30 * fmax(1.0, fabs(lower)); it++) {
+        const double h = (upper - lower) * (1.0 / 17.0);
+        const double x = fma((double)(j + 1), h, lower);
+        const uint64_t neg = __ballot(horner(p, degree, x) <= 0);
+        const int k = __popcll((neg >> (lane & 48)) & 0xffffull);
+        const double nl = k == 0 ? lower : fma((double)k, h, lower);
+        const double nu = k == 16 ? upper : fma((double)(k + 1), h, lower);
+        if (nl == lower && nu == upper) break;
+        lower = nl;
+        upper = nu;
+      }
+      if (lower != upper) {
+        double pd[4];
+        for (int i = 0; i < degree; i++) pd[i] = (i + 1) * p[i + 1];
+        const double blo = fmin(lower, upper), bhi = fmax(lower, upper);
+        double x = 0.5 * (lower + upper);
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+          const double f = horner(p, degree, x), df = horner(pd, degree - 1, x);
+          if (df != 0) x = fmin(bhi, fmax(blo, x - f / df));
+        }
+        lower = x;
+      }
+      my_root = lower;
+      my_has = 1;
+    } else if (fmx == 0) {
+      my_root = mx;
+      my_has = 1;
+    }
+  }
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+__device__ int solve_poly_level_wave(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
+  double my_root;
+  int my_has;
+  solve_poly_level_wave_lane(p, degree, der_roots, n_der, my_root, my_has);
+  int n = 0;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; s2++) {
+    const double r = readlane_f64(my_root, 16 * s2);
+    if (__builtin_amdgcn_readlane(my_has, 16 * s2)) roots[n++] = r;
+  }
+  return n;
+}
+
+template <bool WAVE>
 __device__ int solve_quartic_approx(const double* p4, double* roots, int sub) {
   // derivative chain: p4 (deg 4) -> p3 -> p2 -> p1 (linear)
   double d3[4], d2[3], d1[2];
@@ -401,12 +509,20 @@ __device__ int solve_quartic_approx(const double* p4, double* roots, int sub) {
     r1[0] = -d1[0] / d1[1];
     n1 = 1;
   }
-  const int n2 = solve_poly_level(d2, 2, r1, n1, r2, sub);
-  const int n3 = solve_poly_level(d3, 3, r2, n2, r3, sub);
-  return solve_poly_level(p4, 4, r3, n3, roots, sub);
+  if constexpr (WAVE) {
+    const int n2 = solve_poly_level_wave(d2, 2, r1, n1, r2);
+    const int n3 = solve_poly_level_wave(d3, 3, r2, n2, r3);
+    return solve_poly_level_wave(p4, 4, r3, n3, roots);
+  } else {
+    const int n2 = solve_poly_level(d2, 2, r1, n1, r2, sub);
+    const int n3 = solve_poly_level(d3, 3, r2, n2, r3, sub);
+    return solve_poly_level(p4, 4, r3, n3, roots, sub);
+  }
 }
 
-__device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, const M3& R, M3* out, int sub) {
+template <bool WAVE>
+__device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, const M3& R, M3* out, int sub,
+                                     uint64_t* stamps = nullptr) {
   const V3 R_t_3 = v_scale(t, 1.0 / sqrt(v_dot(t, t)));
   const V3 e_x = {{1, 0, 0}};
   V3 R_t_1 = v_sub(e_x, v_scale(R_t_3, v_dot(e_x, R_t_3)));
@@ -485,10 +601,49 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
     a4 += v_dot(c2, c2);
   }
   const double poly[5] = {a1, 2 * a2 - 4 * a0, 3 * a3 - 3 * a1, 4 * a4 - 2 * a2, -a3};
-  double roots[4];
-  const int n_roots = solve_quartic_approx(poly, roots, sub);
+  if (stamps) stamps[10] = wall_clock64();
   double minimum = 0;
   int n_minima = 0;
+  if constexpr (WAVE) {
+    // the quartic's brackets on their lane groups; each group tests its own root
+    // (second-derivative sign, distance from t_initial: upstream's loop body) and
+    // the results are gathered in bracket order (= upstream's root order)
+    double d3[4], d2[3], d1[2];
+    for (int i = 0; i < 4; i++) d3[i] = (i + 1) * poly[i + 1];
+    for (int i = 0; i < 3; i++) d2[i] = (i + 1) * d3[i + 1];
+    for (int i = 0; i < 2; i++) d1[i] = (i + 1) * d2[i + 1];
+    double r1[1], r2[2], r3[3];
+    int n1 = 0;
+    if (!(fabs(d1[0]) > 1000 * fabs(d1[1]))) {
+      r1[0] = -d1[0] / d1[1];
+      n1 = 1;
+    }
+    const int n2 = solve_poly_level_wave(d2, 2, r1, n1, r2);
+    if (stamps) stamps[11] = wall_clock64();
+    const int n3 = solve_poly_level_wave(d3, 3, r2, n2, r3);
+    if (stamps) stamps[12] = wall_clock64();
+    double rt;
+    int has;
+    solve_poly_level_wave_lane(poly, 4, r3, n3, rt, has);
+    if (stamps) stamps[13] = wall_clock64();
+    int is_min = 0;
+    if (has) {
+      const double t1 = rt, t2 = t1 * t1, t3 = t1 * t2, t4 = t1 * t3, t5 = t1 * t4;
+      if (a2 - 2 * a0 + (3 * a3 - 6 * a1) * t1 + (6 * a4 - 8 * a2 + 10 * a0) * t2 + (-8 * a3 + 6 * a1) * t3 +
+              (-6 * a4 + 3 * a2) * t4 + a3 * t5 >= 0)
+        is_min = fabs(2 * atan(rt) - t_initial) > 0.1;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) {
+      const double r = readlane_f64(rt, 16 * s2);
+      if (__builtin_amdgcn_readlane(is_min, 16 * s2)) {
+        minimum = r;
+        n_minima++;
+      }
+    }
+  } else {
+  double roots[4];
+  const int n_roots = solve_quartic_approx<false>(poly, roots, sub);
   for (int i = 0; i < n_roots; i++) {
     const double t1 = roots[i], t2 = t1 * t1, t3 = t1 * t2, t4 = t1 * t3, t5 = t1 * t4;
     if (a2 - 2 * a0 + (3 * a3 - 6 * a1) * t1 + (6 * a4 - 8 * a2 + 10 * a0) * t2 + (-8 * a3 + 6 * a1) * t3 +
@@ -500,6 +655,8 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
       }
     }
   }
+  }
+  if (stamps) stamps[14] = wall_clock64();
   if (n_minima != 1) return false;
   const double tm = minimum;
   M3 Rb;
@@ -512,8 +669,10 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
 }
 
 // estimate_tag_pose: writes R (row-major), t and the winning error.
-// sub: this lane's index in the detection's quad (see solve_poly_level); all
-// four lanes return the same pose.
+// WAVE = false: sub is this lane's index in the detection's quad (see
+// solve_poly_level); all four lanes return the same pose.  WAVE = true: the whole
+// wave works on one detection (solve_poly_level_wave); every lane returns it.
+template <bool WAVE = false>
 __device__ void estimate_tag_pose(const double H[9], const double corners[4][2], double fx, double fy, double cx,
                                   double cy, double tagsize, double* R_out, double* t_out, double* err_out, int sub,
                                   uint64_t* stamps = nullptr) {
@@ -556,7 +715,7 @@ __device__ void estimate_tag_pose(const double H[9], const double corners[4][2],
   M3 R2;
   V3 t2 = {{0, 0, 0}};
   double err2 = HUGE_VAL;
-  const bool amb = fix_pose_ambiguities(v, p, t1, R1, &R2, sub);
+  const bool amb = fix_pose_ambiguities<WAVE>(v, p, t1, R1, &R2, sub, stamps);
   if (stamps) stamps[3] = wall_clock64();
   if (amb) err2 = orthogonal_iteration(v, p, &t2, &R2, 50, &k2);
   if (stamps) {

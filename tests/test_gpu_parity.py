@@ -196,14 +196,17 @@ def _pose_close(a_R, a_t, b_R, b_t, tol):
     return np.abs(np.asarray(a_R) - np.asarray(b_R)).max() <= tol and np.abs(np.asarray(a_t) - np.asarray(b_t)).max() <= tol
 
 
-@pytest.mark.parametrize("frame", [0, 1])
-def test_pose_parity_720p(gpu, oracle_mod, frame):
+@pytest.mark.parametrize("frame,batch", [(0, 1), (1, 1), (2, 8)])
+def test_pose_parity_720p(gpu, oracle_mod, frame, batch):
     """GPU pose of every detection vs the oracle pose of the oracle's detection
-    with the same id: within 1e-4 (north star float tolerance)."""
+    with the same id: within 1e-4 (north star float tolerance).  batch 1: the
+    latency mode's k_pose (a wave per detection, parallel bracket search for the
+    quartic's roots); batch 8: four lanes per detection (safeguarded Newton as
+    upstream)."""
     from ros_vision_amd import synth
     cam = gpu.TEST_CAMERA
     yuyv, _, _ = synth.stream_frame(1280, 720, frame)
-    det = gpu.GpuDetector(1280, 720)
+    det = gpu.GpuDetector(1280, 720, max_batch=batch)
     dets = det.detect(yuyv)
     poses = det.poses()
     assert len(poses) == len(dets) > 0
@@ -225,6 +228,28 @@ def test_pose_parity_720p(gpu, oracle_mod, frame):
         R, t, _, _, _ = oracle_mod.estimate_tag_pose(d.H, d.p, cam.fx, cam.fy, cam.cx, cam.cy)
         assert _pose_close(p.R, p.t, R, t, 1e-9), d.id
     print("pose worst |diff| vs oracle detections: %.3g" % worst)
+
+
+def test_wave_pose_matches_quad_pose(gpu):
+    """The latency mode's k_pose (a wave per detection, parallel bracket search for
+    the quartic's roots) equals the throughput mode's (four lanes per detection,
+    upstream's safeguarded Newton) to 1e-9 on every detection of several frames."""
+    import torch
+    from ros_vision_amd import synth
+    frames = np.stack([synth.stream_frame(1280, 720, f)[0] for f in range(3, 11)])
+    t = torch.from_numpy(frames).cuda()
+    quad = gpu.GpuDetector(1280, 720, max_batch=8)
+    quad.detect_device(t.data_ptr(), frames[0].nbytes, 8)
+    wave = gpu.GpuDetector(1280, 720, max_batch=1)
+    n = 0
+    for f in range(8):
+        a = wave.detect(frames[f])
+        assert [d.id for d in a] == [d.id for d in quad.detections(f)]
+        for pa, pb in zip(wave.poses(), quad.poses(f)):
+            assert _pose_close(pa.R, pa.t, pb.R, pb.t, 1e-9), (pa.id, pa.t, pb.t)
+            assert pa.err == pytest.approx(pb.err, rel=1e-9, abs=1e-15)
+            n += 1
+    assert n >= 80
 
 
 def test_pose_disabled_and_camera_to_robot(gpu):
@@ -300,7 +325,8 @@ def test_distortion_variants(gpu, oracle_mod, dist):
     assert sorted(d.id for d in dets) == sorted(t[0] for t in truth)
 
 
-@pytest.mark.parametrize("batch,timed", [(8, "k_blob"), (8, "k_boundary"), (1, "k_blob_small"), (1, "k_pose")])
+@pytest.mark.parametrize("batch,timed", [(8, "k_blob"), (8, "k_boundary"), (1, "k_blob_small"), (8, "k_pose"),
+                                         (1, "k_decode")])
 def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     """The bench's launch modes give identical detections: hipGraph replay, the
     split graph around a timed kernel (fence-free events between three graphs; on

@@ -28,3 +28,7 @@ for name, base in (("k_blob_small", 64), ("k_blob", 80), ("k_decode", 128)):
             row.append("%d:%.2fus(x%d)" % (k, t / n / 100.0, n))
     print(name, " ".join(row))
 print("pose phases (us): polar3 %.2f  OI-1 %.2f  ambiguity %.2f  OI-2 %.2f" % tuple(np.diff(p[16:21]) / 100.0))
+a = p[16 + 2]
+print("ambiguity detail (us): setup %.2f  deg2 %.2f  deg3 %.2f  deg4 %.2f  minima %.2f  rest %.2f" % (
+    (p[26] - a) / 100.0, (p[27] - p[26]) / 100.0, (p[28] - p[27]) / 100.0, (p[29] - p[28]) / 100.0,
+    (p[30] - p[29]) / 100.0, (p[19] - p[30]) / 100.0))
