@@ -962,6 +962,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
     const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
     const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
+    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);  // (same round trip)
     const uint32_t incl_e = block_incl_scan(ne, s_wsum, &tot_e, 16);
     if (tid < ntb) s_tpre[tid] = incl_e - ne;
     if (tid == 0) s_tpre[ntb] = tot_e;
@@ -986,7 +987,6 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
         b.pent_cnt[e] = kGrpFallback;  // beyond the register cache: k_group reserves per point
       }
     }
-    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
     for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
     __syncthreads();
     if (tid == 0) {
@@ -1021,27 +1021,48 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __syncthreads();
   stamp(2);
   if (n <= 1024) {
-    // rank sort (keys are unique: the slot rides in the low bits); t_key is free
-    // once the lookup table has been written out above.  P = 1024 / n threads per
-    // key, each counting the smaller keys of a 1/P slice of the list (a frame's
-    // ~400 pairs: 2 threads per key, half the serial LDS reads)
-    const int P = (int)(1024 / (n ? n : 1u));
-    uint32_t* s_rank = reinterpret_cast<uint32_t*>(t_key + 2048);
-    if (tid < (int)n) s_rank[tid] = 0;
-    __syncthreads();
-    if (tid < P * (int)n) {
-      const int i = tid % (int)n, h = tid / (int)n;
-      const uint64_t key = s_list[i];
-      const int j1 = (int)(((uint32_t)h + 1) * n / (uint32_t)P);
-      int j = (int)((uint32_t)h * n / (uint32_t)P);
-      uint32_t r = 0;
-      for (; j + 4 <= j1; j += 4)
-        r += (s_list[j] < key) + (s_list[j + 1] < key) + (s_list[j + 2] < key) + (s_list[j + 3] < key);
-      for (; j < j1; j++) r += s_list[j] < key;
-      if (r) atomicAdd(&s_rank[i], r);
+    // keys are unique (the slot rides in the low bits).  Each wave sorts its 64
+    // keys in registers (bitonic, lane exchanges), writes the sorted run, and a
+    // key's rank is its position in its own run plus, for every other run, the
+    // number of smaller keys there (binary searches, all runs at once); t_key is
+    // free once the lookup table has been written out above
+    const int nw = (int)((n + 63) >> 6);
+    const int w = tid >> 6;
+    const uint32_t ln = lane_id();
+    uint64_t* run = t_key + 2048;  // [nw][64] sorted runs (~0 padding past n)
+    if (w < nw) {
+      uint64_t key = s_list[tid];  // ~0 past n (filled above)
+#pragma unroll
+      for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const uint64_t o = __shfl_xor(key, j);
+          const bool up = (ln & k) == 0, lower = (ln & j) == 0;
+          // keep the smaller of the pair in the lower lane of an ascending block
+          key = ((key < o) == (lower == up)) ? key : o;
+        }
+      }
+      run[w * 64 + ln] = key;
     }
     __syncthreads();
-    if (tid < (int)n) t_key[s_rank[tid]] = s_list[tid];
+    if (tid < (int)n) {
+      const uint64_t key = s_list[tid];
+      uint32_t r = 0;
+      uint32_t pos[16];
+#pragma unroll
+      for (int v = 0; v < 16; v++) pos[v] = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+#pragma unroll
+        for (int v = 0; v < 16; v++)
+          if (v < nw && run[v * 64 + pos[v] + step - 1] < key) pos[v] += step;
+      }
+#pragma unroll
+      for (int v = 0; v < 16; v++)
+        if (v < nw) r += pos[v] + (run[v * 64 + pos[v]] < key ? 1u : 0u);
+      // (in its own run the key itself is not counted: equal, not smaller)
+      t_key[r] = key;
+    }
     __syncthreads();
     if (tid < (int)n) s_list[tid] = t_key[tid];
     __syncthreads();
