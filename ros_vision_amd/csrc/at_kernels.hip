@@ -721,7 +721,7 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
 template <bool KEPT>
-__global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
   // points staged in LDS up to kBndStage (typical tiles hold ~0.7 points per
@@ -811,6 +811,10 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       }
     }
     uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
+    // run heads of the four directions: their first hash probes are issued
+    // together (one LDS round trip instead of four); a key not at its home slot
+    // (first sighting in the tile, or a collision) takes the probing insert
+    uint32_t hl[4];  // run length at run heads, 0 elsewhere (keys: pk[dir] >> 24)
 #pragma unroll
     for (int dir = 0; dir < 4; dir++) {
       const bool has = pk[dir] != 0;
@@ -821,10 +825,17 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       const uint64_t prev = wave_shr1_u64(r01);
       const bool same = has && lane > 0 && prev == r01;
       const uint64_t same_mask = __ballot(same);
-      if (has && !same) {
-        const uint32_t len = run_len(same_mask, lane);
-        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) bnd_spill(b, f, r01, len);  // LDS table full
-      }
+      hl[dir] = has && !same ? run_len(same_mask, lane) : 0u;
+    }
+    uint64_t home[4];
+#pragma unroll
+    for (int dir = 0; dir < 4; dir++) home[dir] = hl[dir] ? s_pkey[mix_hash(pk[dir] >> 24) & (kLdsPairSlots - 1)] : 0ull;
+#pragma unroll
+    for (int dir = 0; dir < 4; dir++) {
+      if (!hl[dir]) continue;
+      const uint64_t r01 = pk[dir] >> 24;
+      if (home[dir] == r01) atomicAdd(s_pcnt + (mix_hash(r01) & (kLdsPairSlots - 1)), hl[dir]);
+      else if (!lds_pair_add(s_pkey, s_pcnt, r01, hl[dir])) bnd_spill(b, f, r01, hl[dir]);  // LDS table full
     }
     // wave-aggregated append of the points into the LDS staging buffer
     uint32_t wbase = 0;
