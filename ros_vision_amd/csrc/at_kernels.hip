@@ -605,13 +605,39 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   uint32_t* size = b.size + fo;
   const uint32_t n = b.nlroot[tl];
   const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-  for (uint32_t k = threadIdx.x; k < n; k += 64) {
-    const uint32_t l = lr[k];
-    const uint32_t r = g_find(par, l);
-    if (r != l) {
-      par[l] = r;  // unions are over: a concurrent find sees the old parent or r, both lead to r
-      const uint32_t cnt = size[l];
-      atomicAdd(size + r, cnt);  // result unused: no round trip (size[l] is dead from here on)
+  // four local roots per lane at a time, their finds in lockstep (independent
+  // loads issued together) and each count loaded with the first parent
+  constexpr int kJ = 4;
+  for (uint32_t k0 = threadIdx.x; k0 < n; k0 += 64 * kJ) {
+    uint32_t l[kJ], p[kJ], c[kJ], r[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; j++) l[j] = k0 + 64 * j < n ? lr[k0 + 64 * j] : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < kJ; j++) {
+      p[j] = l[j] != 0xffffffffu ? g_load(par + l[j]) : l[j];
+      c[j] = l[j] != 0xffffffffu ? size[l[j]] : 0u;
+      r[j] = l[j];
+    }
+    bool more = true;
+    while (more) {
+      more = false;
+#pragma unroll
+      for (int j = 0; j < kJ; j++) {
+        if (p[j] != r[j]) {
+          r[j] = p[j];
+          more = true;
+        }
+      }
+      if (!more) break;
+#pragma unroll
+      for (int j = 0; j < kJ; j++) p[j] = l[j] != 0xffffffffu ? g_load(par + r[j]) : r[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kJ; j++) {
+      if (l[j] != 0xffffffffu && r[j] != l[j]) {
+        par[l[j]] = r[j];  // unions are over: a concurrent find sees the old parent or r, both lead to r
+        atomicAdd(size + r[j], c[j]);  // result unused: no round trip (size[l] is dead from here on)
+      }
     }
   }
 }
@@ -629,10 +655,18 @@ __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
   const uint32_t* size = b.size + fo;
   const uint32_t n = b.nlroot[tl];
   const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-  for (uint32_t k = threadIdx.x; k < n; k += 64) {
-    const uint32_t l = lr[k];
-    const uint32_t r = par[l];
-    par[l] = r | (size[r] >= 25 ? kKeptBit : 0u);
+  constexpr int kJ = 4;  // four per lane at a time: three round trips for all of them
+  for (uint32_t k0 = threadIdx.x; k0 < n; k0 += 64 * kJ) {
+    uint32_t l[kJ], r[kJ], z[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; j++) l[j] = k0 + 64 * j < n ? lr[k0 + 64 * j] : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < kJ; j++) r[j] = l[j] != 0xffffffffu ? par[l[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < kJ; j++) z[j] = l[j] != 0xffffffffu ? size[r[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < kJ; j++)
+      if (l[j] != 0xffffffffu) par[l[j]] = r[j] | (z[j] >= 25 ? kKeptBit : 0u);
   }
 }
 
