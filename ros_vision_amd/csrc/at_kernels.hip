@@ -953,6 +953,14 @@ constexpr int kGrpEnt = 128;  // tile entries with an LDS cursor in k_group (typ
 constexpr uint32_t kGrpDrop = 0xfffffffeu, kGrpFallback = 0xffffffffu;
 constexpr int kPairsEntCache = 4;  // entries per thread whose hash slot k_pairs keeps in registers
 
+// LDS: the frame's pair hash packs key (40 bits) and point count (24 bits) in one
+// word (32 KB); the sort list of a frame's <= 1024 pairs and its sorted runs take
+// 8 KB each; frames with more pairs sort their list in global memory (b.plist).
+// 45 KB per workgroup (was 84): a batch's k_pairs finds a CU sooner while other
+// batches' kernels fill the GPU.
+constexpr int kPairsLdsList = 1024;
+constexpr int kCntBits = 24;
+constexpr uint64_t kCntMask = (1ull << kCntBits) - 1;
 __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
@@ -960,30 +968,29 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     if (probe && f == 0 && tid == 0) b.probe[i] = wall_clock64();
   };
   stamp(0);
-  __shared__ uint64_t t_key[kHashSlots];
-  __shared__ uint32_t t_cnt[kHashSlots];
-  __shared__ uint64_t s_list[kMaxPairs];
+  __shared__ uint64_t t_hash[kHashSlots];  // (key << 24) | count; 0 = empty
+  __shared__ uint64_t s_list[kPairsLdsList];
+  __shared__ uint64_t s_aux[kPairsLdsList];
   __shared__ uint32_t s_n, s_full, s_np;
   __shared__ uint32_t s_wsum[16];
-  for (int i = tid; i < kHashSlots; i += 1024) {
-    t_key[i] = 0;
-    t_cnt[i] = 0;
-  }
+  for (int i = tid; i < kHashSlots; i += 1024) t_hash[i] = 0;
   if (tid == 0) { s_n = 0; s_full = 0; s_np = 0; }
   __syncthreads();
-  // merge the per-tile pair histograms of k_boundary in LDS: wave w takes
-  // tiles w, w + 16, ...; then the overflow entries of crowded tiles
+  // merge the per-tile pair histograms of k_boundary in LDS (a frame's pairs hold
+  // fewer than 2^24 points each: the count never carries into the key)
   auto merge = [&](uint64_t key, uint32_t cnt) -> uint32_t {
     uint32_t h = (uint32_t)mix_hash(key) & (kHashSlots - 1);
     for (int probe = 0; probe < kHashSlots; probe++) {
-      const uint64_t k = t_key[h];
-      if (k == key) {
-        atomicAdd(&t_cnt[h], cnt);
+      const uint64_t w = t_hash[h];
+      if (w != 0 && (w >> kCntBits) == key) {
+        atomicAdd((unsigned long long*)&t_hash[h], (unsigned long long)cnt);
         return h;
-      } else if (k == 0) {
-        const uint64_t prev = atomicCAS((unsigned long long*)&t_key[h], 0ull, (unsigned long long)key);
-        if (prev == 0 || prev == key) {
-          atomicAdd(&t_cnt[h], cnt);
+      } else if (w == 0) {
+        const uint64_t prev =
+            atomicCAS((unsigned long long*)&t_hash[h], 0ull, (unsigned long long)((key << kCntBits) | cnt));
+        if (prev == 0) return h;
+        if ((prev >> kCntBits) == key) {
+          atomicAdd((unsigned long long*)&t_hash[h], (unsigned long long)cnt);
           return h;
         }
       }
@@ -1041,11 +1048,14 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   }
   __syncthreads();
   stamp(1);
+  uint64_t* glist = b.plist + (size_t)f * kMaxPairs;
   for (int s = tid; s < kHashSlots; s += 1024) {
-    const uint64_t k = t_key[s];
-    if (k) {
+    const uint64_t w = t_hash[s];
+    if (w) {
       const uint32_t i = atomicAdd(&s_n, 1u);
-      if (i < kMaxPairs) s_list[i] = (k << kHashBits) | (uint64_t)s;
+      const uint64_t lk = ((w >> kCntBits) << kHashBits) | (uint64_t)s;
+      if (i < (uint32_t)kPairsLdsList) s_list[i] = lk;
+      else if (i < (uint32_t)kMaxPairs) glist[i] = lk;
     }
   }
   __syncthreads();
@@ -1057,26 +1067,34 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   }
   // the lookup table used by k_group: keys of every slot (0 = empty)
   for (int s = tid; s < kHashSlots; s += 1024) {
-    b.ht_key[(size_t)f * kHashSlots + s] = t_key[s];
-    b.ht_cnt[(size_t)f * kHashSlots + s] = t_cnt[s];
+    const uint64_t w = t_hash[s];
+    b.ht_key[(size_t)f * kHashSlots + s] = w >> kCntBits;
+    b.ht_cnt[(size_t)f * kHashSlots + s] = (uint32_t)(w & kCntMask);
   }
   int np2 = 64;
   while (np2 < (int)n) np2 <<= 1;
-  for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
+  const bool big = n > (uint32_t)kPairsLdsList;
+  uint64_t* list = big ? glist : s_list;
+  if (big) {
+    // more pairs than the LDS list holds (dense texture): the whole list in
+    // global memory (one workgroup's own scratch) and a bitonic sort there
+    for (int i = tid; i < kPairsLdsList; i += 1024) glist[i] = s_list[i];
+  }
+  for (int i = (int)n + tid; i < np2; i += 1024) list[i] = ~0ull;
   __syncthreads();
   stamp(2);
-  if (n <= 1024) {
+  if (!big) {
     // keys are unique (the slot rides in the low bits).  Each wave sorts its 64
     // keys in registers (bitonic, lane exchanges), writes the sorted run, and a
     // key's rank is its position in its own run plus, for every other run, the
-    // number of smaller keys there (binary searches, all runs at once); t_key is
-    // free once the lookup table has been written out above
+    // number of smaller keys there (binary searches, all runs at once)
     const int nw = (int)((n + 63) >> 6);
     const int w = tid >> 6;
     const uint32_t ln = lane_id();
-    uint64_t* run = t_key + 2048;  // [nw][64] sorted runs (~0 padding past n)
+    uint64_t* run = s_aux;  // [nw][64] sorted runs (~0 padding past n)
+    const uint64_t key0 = s_list[tid];  // ~0 past n (filled above)
     if (w < nw) {
-      uint64_t key = s_list[tid];  // ~0 past n (filled above)
+      uint64_t key = key0;
 #pragma unroll
       for (int k = 2; k <= 64; k <<= 1) {
 #pragma unroll
@@ -1091,7 +1109,6 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     }
     __syncthreads();
     if (tid < (int)n) {
-      const uint64_t key = s_list[tid];
       uint32_t r = 0;
       uint32_t pos[16];
 #pragma unroll
@@ -1100,26 +1117,29 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       for (int step = 32; step > 0; step >>= 1) {
 #pragma unroll
         for (int v = 0; v < 16; v++)
-          if (v < nw && run[v * 64 + pos[v] + step - 1] < key) pos[v] += step;
+          if (v < nw && run[v * 64 + pos[v] + step - 1] < key0) pos[v] += step;
       }
 #pragma unroll
       for (int v = 0; v < 16; v++)
-        if (v < nw) r += pos[v] + (run[v * 64 + pos[v]] < key ? 1u : 0u);
+        if (v < nw) r += pos[v] + (run[v * 64 + pos[v]] < key0 ? 1u : 0u);
       // (in its own run the key itself is not counted: equal, not smaller)
-      t_key[r] = key;
+      s_list[r] = key0;  // every key was read before the barrier above
     }
     __syncthreads();
-    if (tid < (int)n) s_list[tid] = t_key[tid];
-    __syncthreads();
   } else {
-    block_bitonic_sort<uint64_t, 1024>(s_list, np2);
+    block_bitonic_sort<uint64_t, 1024>(glist, np2);
   }
   stamp(3);
   // counts in rank order (straight from the hash slots), exclusive scan -> offsets;
   // each thread owns 4 consecutive ranks
   const int i0 = tid * 4;
-  auto cnt_at = [&](int i) -> uint32_t { return i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u; };
+  auto cnt_at = [&](int i) -> uint32_t {
+    return i < (int)n ? (uint32_t)(t_hash[list[i] & (kHashSlots - 1)] & kCntMask) : 0u;
+  };
   const uint32_t c0 = cnt_at(i0), c1 = cnt_at(i0 + 1), c2 = cnt_at(i0 + 2), c3 = cnt_at(i0 + 3);
+  uint32_t sl[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) sl[k] = i0 + k < (int)n ? (uint32_t)(list[i0 + k] & (kHashSlots - 1)) : 0u;
   const uint32_t tsum = c0 + c1 + c2 + c3;
   const uint32_t incl = wave_incl_scan(tsum, AddOp(), 0u);
   const uint32_t lane = lane_id();
@@ -1134,7 +1154,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   // work-list appends by size class: LDS slots, then one global atomic per
   // class per workgroup
   __shared__ uint32_t s_ccnt[kNumCls], s_cbase[kNumCls];
-  __syncthreads();  // s_n / s_full / s_wsum reads done
+  __syncthreads();  // s_n / s_full / s_wsum / t_hash reads done
   if (tid < kNumCls) s_ccnt[tid] = 0;
   __syncthreads();
   int cls[4];
@@ -1151,11 +1171,17 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __syncthreads();
   if (tid < kNumCls) s_cbase[tid] = s_ccnt[tid] ? atomicAdd(b.ncls + tid, s_ccnt[tid]) : 0u;
   __syncthreads();
+  // segment bases of the tiles' first kGrpEnt entries: per pair slot its segment
+  // offset (kGrpDrop outside the size bounds) and an LDS cursor, over the hash
+  // table (every read of it is done); the cursors' final values seed k_group's
+  // per-point reservations
+  uint32_t* t_off = reinterpret_cast<uint32_t*>(t_hash);
+  uint32_t* t_cur = t_off + kHashSlots;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
     if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      const uint32_t slot = sl[k];
       b.ht_rank[(size_t)f * kHashSlots + slot] = (uint32_t)i;
       b.ht_off[(size_t)f * kHashSlots + slot] = offs[k];
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
@@ -1163,19 +1189,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
       if (cls[k] >= 0)
         b.work[(size_t)cls[k] * b.wcap + s_cbase[cls[k]] + lslot[k]] = ((uint32_t)f << 16) | (uint32_t)i;
-    }
-  }
-  // segment bases of the tiles' first kGrpEnt entries (LDS cursors per pair slot;
-  // t_key's storage is free since the sort), then the cursors' final values seed
-  // k_group's per-point reservations
-  uint32_t* t_off = reinterpret_cast<uint32_t*>(t_key);
-  uint32_t* t_cur = t_off + kHashSlots;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int i = i0 + k;
-    if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
-      t_off[slot] = offs[k];
+      t_off[slot] = cs[k] >= g.min_cluster && cs[k] <= g.max_cluster ? offs[k] : kGrpDrop;
       t_cur[slot] = 0;
     }
   }
@@ -1183,19 +1197,15 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 #pragma unroll
   for (int k = 0; k < kPairsEntCache; k++) {
     if (c_slot[k] != 0xffffffffu && c_lds[k]) {
-      const uint32_t tc = t_cnt[c_slot[k]];
-      const bool keep = tc >= g.min_cluster && tc <= g.max_cluster;
-      b.pent_cnt[c_idx[k]] = keep ? t_off[c_slot[k]] + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
+      const uint32_t o = t_off[c_slot[k]];
+      b.pent_cnt[c_idx[k]] = o != kGrpDrop ? o + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
-    if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
-      b.ht_cur[(size_t)f * kHashSlots + slot] = t_cur[slot];
-    }
+    if (i < (int)n) b.ht_cur[(size_t)f * kHashSlots + sl[k]] = t_cur[sl[k]];
   }
   stamp(5);
 }
