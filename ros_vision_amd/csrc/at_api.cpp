@@ -124,7 +124,7 @@ struct at_detector {
   int device;
   int nblobwg;
   hipStream_t st;
-  hipStream_t st2;          // fork/join branch for the small-blob kernel
+  hipStream_t st2;          // fork/join branch for the large-blob kernel (latency mode)
   hipEvent_t ev_fork, ev_join;
   DevBufs d;
   std::vector<void*> allocs;

@@ -3761,8 +3761,11 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     hipError_t e;
     if ((e = hipEventRecord(fork, st))) return e;
     if ((e = hipStreamWaitEvent(st2, fork, 0))) return e;
-    blob_small(st2);
-    blob_large(st);
+    // the small-blob kernel stays on the main stream (no cross-queue wait before
+    // it); the large-blob kernel, which finishes first, is the forked one, so the
+    // join's wait is on a signal that has usually fired: ~5 us less at B = 1
+    blob_small(st);
+    blob_large(st2);
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }
