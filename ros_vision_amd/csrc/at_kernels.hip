@@ -409,7 +409,11 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       if (bb == 0 && T(pr - 1, pc + 1) == 0) tR = s_par[slot_of<TWD>(bty - 1, btx, 2)];
     }
     // the left neighbour's targets (same wave: rows never straddle waves)
-    const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
+    // (DPP wave_shr:1 moves: lane 0 / the first lane of a block row never uses them)
+    const uint32_t pUL = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tUL, 0x138, 0xf, 0xf, false);
+    const uint32_t pU = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tU, 0x138, 0xf, 0xf, false);
+    const uint32_t pUR = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tUR, 0x138, 0xf, 0xf, false);
+    const uint32_t pR = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tR, 0x138, 0xf, 0xf, false);
     __syncthreads();
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
