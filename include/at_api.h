@@ -217,6 +217,17 @@ int at_gp_copy(at_detector *d, int frame, float *dst, size_t count);
 int at_gp_preprocess_device(const uint8_t *bgr, int width, int height, float *out, int out_width, int out_height,
                             int channels, void *stream);
 
+/* The annotated image on the GPU: the node's outlined frame
+ * (apriltag_utils.cu:54-79, drawn on the host with cv::line / cv::putText by
+ * apriltags_cuda_detector.cu:514-518) drawn onto a device-resident BGR8 image of
+ * the detector's geometry (width x height x 3, row-major): per detection the four
+ * sides (0-1 green, 0-3 red, 1-2 / 2-3 blue; corners truncated to int as
+ * cv::Point does) and the id centred on c, 2-px segments.  Pixel-identical to
+ * node/at_node.cpp's draw_detection_outlines (its digit glyphs, not OpenCV's
+ * Hershey font).  `dets` as at_collect returned them (host memory).  Runs on the
+ * detector's stream and returns when the image is drawn. */
+int at_draw_outlines_device(at_detector *d, const at_detection *dets, int n, uint8_t *bgr);
+
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);
 

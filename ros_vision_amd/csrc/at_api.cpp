@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <string>
 #include <vector>
 
 #include "../../include/at_api.h"
@@ -25,6 +26,7 @@ hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint3
                             int Hd, hipStream_t st);
 hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd, hipStream_t st);
 hipError_t launch_gp_preprocess(const uint8_t* src, int w, int h, float* out, int ow, int oh, int c, hipStream_t st);
+hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bgr, int W, int H, hipStream_t st);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt);
@@ -157,6 +159,10 @@ struct at_detector {
   double stage_ms[kNumStages];
   long stage_batches;
   double host_wait_us, host_tail_us;  // cumulative time of at_collect in the event wait / the host tail
+  // annotated image (at_draw_outlines_device): segments, last-writer plane (lazily allocated)
+  DrawPrim* d_prims;
+  size_t prims_cap;
+  uint32_t* d_last;
 };
 
 static int hip_fail(hipError_t e) {
@@ -236,6 +242,8 @@ void at_destroy(at_detector* d) {
   if (d->h_ftab) (void)hipHostFree(d->h_ftab);
   if (d->h_ctrl) (void)hipHostFree(d->h_ctrl);
   if (d->h_dets) (void)hipHostFree(d->h_dets);
+  if (d->d_prims) (void)hipFree(d->d_prims);
+  if (d->d_last) (void)hipFree(d->d_last);
   if (d->ev_done) (void)hipEventDestroy(d->ev_done);
   if (d->ev_ext) (void)hipEventDestroy(d->ev_ext);
   for (int i = 0; i <= kNumStages; i++)
@@ -844,6 +852,79 @@ int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const d
                    [](const at_tag_detection& a, const at_tag_detection& b) { return a.distance < b.distance; });
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
+}
+
+// ---- annotated image ------------------------------------
+// The segments of node/at_node.cpp's draw_detection_outlines, in its drawing order:
+// per detection the four sides (apriltag_utils.cu:58-65: corners truncated to int
+// as cv::Point does; 0-1 green, 0-3 red, 1-2 and 2-3 blue), then the id's digit
+// strokes centred on c (:67-77).  The digit strokes are the node's.
+static void outline_prims(const at_detection* dets, int n, std::vector<DrawPrim>* out) {
+  static const uint8_t kGreen[3] = {0, 0xff, 0}, kRed[3] = {0, 0, 0xff}, kBlue[3] = {0xff, 0, 0},
+                       kText[3] = {0xff, 0x99, 0};
+  static const std::vector<std::vector<std::pair<int, int>>> kDigits[10] = {
+      {{{0, 1}, {1, 0}, {3, 0}, {4, 1}, {4, 7}, {3, 8}, {1, 8}, {0, 7}, {0, 1}}},
+      {{{1, 2}, {2, 0}, {2, 8}}, {{1, 8}, {3, 8}}},
+      {{{0, 1}, {1, 0}, {3, 0}, {4, 1}, {4, 3}, {0, 8}, {4, 8}}},
+      {{{0, 0}, {4, 0}, {2, 3}, {3, 3}, {4, 4}, {4, 7}, {3, 8}, {1, 8}, {0, 7}}},
+      {{{3, 8}, {3, 0}, {0, 5}, {4, 5}}},
+      {{{4, 0}, {0, 0}, {0, 3}, {3, 3}, {4, 4}, {4, 7}, {3, 8}, {0, 8}}},
+      {{{4, 0}, {2, 0}, {0, 3}, {0, 7}, {1, 8}, {3, 8}, {4, 7}, {4, 5}, {3, 4}, {0, 4}}},
+      {{{0, 0}, {4, 0}, {1, 8}}},
+      {{{1, 4}, {0, 3}, {0, 1}, {1, 0}, {3, 0}, {4, 1}, {4, 3}, {3, 4}, {1, 4}, {0, 5}, {0, 7}, {1, 8},
+        {3, 8}, {4, 7}, {4, 5}, {3, 4}}},
+      {{{4, 4}, {1, 4}, {0, 3}, {0, 1}, {1, 0}, {3, 0}, {4, 1}, {4, 5}, {2, 8}, {0, 8}}},
+  };
+  auto seg = [&](double x0, double y0, double x1, double y1, const uint8_t c[3]) {
+    DrawPrim q;
+    q.x0 = x0; q.y0 = y0; q.x1 = x1; q.y1 = y1;
+    q.bgr[0] = c[0]; q.bgr[1] = c[1]; q.bgr[2] = c[2];
+    out->push_back(q);
+  };
+  for (int i = 0; i < n; i++) {
+    const at_detection& d = dets[i];
+    auto P = [&](int k, int c) { return (double)(int)d.p[k][c]; };
+    seg(P(0, 0), P(0, 1), P(1, 0), P(1, 1), kGreen);
+    seg(P(0, 0), P(0, 1), P(3, 0), P(3, 1), kRed);
+    seg(P(1, 0), P(1, 1), P(2, 0), P(2, 1), kBlue);
+    seg(P(2, 0), P(2, 1), P(3, 0), P(3, 1), kBlue);
+    const std::string text = std::to_string(d.id);
+    const double sc = 2.5, adv = 7 * sc;
+    const double tw = adv * text.size() - 2 * sc, th = 8 * sc;
+    const double ox = (int)(d.c[0] - tw / 2), oy = (int)(d.c[1] - th / 2);
+    for (size_t k = 0; k < text.size(); ++k) {
+      if (text[k] < '0' || text[k] > '9') continue;
+      for (const auto& stroke : kDigits[text[k] - '0'])
+        for (size_t t = 1; t < stroke.size(); ++t)
+          seg(ox + k * adv + stroke[t - 1].first * sc, oy + stroke[t - 1].second * sc, ox + k * adv + stroke[t].first * sc,
+              oy + stroke[t].second * sc, kText);
+    }
+  }
+}
+
+int at_draw_outlines_device(at_detector* d, const at_detection* dets, int n, uint8_t* bgr) {
+  if (!d || n < 0 || (n > 0 && !dets) || !bgr) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  std::vector<DrawPrim> prims;
+  outline_prims(dets, n, &prims);
+  if (prims.empty()) return AT_OK;
+  const size_t W = (size_t)d->g.W, H = (size_t)d->g.H;
+  if (!d->d_last) {
+    HIPCHK(hipMalloc((void**)&d->d_last, W * H * 4));
+    HIPCHK(hipMemset(d->d_last, 0, W * H * 4));  // kept zero by the paint pass
+  }
+  if (prims.size() > d->prims_cap) {
+    if (d->d_prims) HIPCHK(hipFree(d->d_prims));
+    d->d_prims = nullptr;
+    d->prims_cap = 0;
+    const size_t cap = std::max<size_t>(1024, prims.size() * 2);
+    HIPCHK(hipMalloc((void**)&d->d_prims, cap * sizeof(DrawPrim)));
+    d->prims_cap = cap;
+  }
+  HIPCHK(hipMemcpyAsync(d->d_prims, prims.data(), prims.size() * sizeof(DrawPrim), hipMemcpyHostToDevice, d->st));
+  HIPCHK(launch_draw(d->d_prims, (int)prims.size(), d->d_last, bgr, (int)W, (int)H, d->st));
+  HIPCHK(hipStreamSynchronize(d->st));
+  return AT_OK;
 }
 
 // ---- shared game-piece preprocessing ---------------------

@@ -165,6 +165,12 @@ struct QuadRecord {
   float corners[4][2];
 };
 
+// One 2-px-thick segment of the annotated image (at_draw_outlines_device).
+struct DrawPrim {
+  double x0, y0, x1, y1;
+  uint8_t bgr[3];
+};
+
 // Device buffers; every per-frame array is [max_batch][per-frame size].
 struct DevBufs {
   const uint8_t* const* frames;   // device table of frame pointers

@@ -3660,6 +3660,64 @@ hipError_t launch_gp_preprocess(const uint8_t* src, int w, int h, float* out, in
 // kt (optional): HIP events bracketing one kernel (kt->stage, kStageNames
 // order) on the stream it runs on -- the live per-launch duration bench.py
 // reports for the roofline; recorded inside the captured graph as well.
+// ---------------------------------------------------------------------------
+// Annotated image on the GPU: the node's outlined frame
+// (apriltag_utils.cu:54-79 -- cv::line of the four sides in green / red / blue /
+// blue and the id text at the centre) drawn straight onto the BGR8 frame in HBM.
+// Primitives are 2-px-thick segments in drawing order (at_api.cpp builds them as
+// node/at_node.cpp's draw_detection_outlines does); a pixel whose centre lies
+// within 1 px of a segment takes that segment's colour, the LAST covering segment
+// winning as in the sequential CPU drawing: pass 1 records the highest covering
+// primitive per pixel (atomicMax), pass 2 lets that primitive paint and clears the
+// record (the scratch plane stays zero between calls).  Same double arithmetic as
+// the CPU code (no contraction): the images are bit-identical.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool seg_box(const DrawPrim& q, int W, int H, int* x0, int* y0, int* bw, int* bh) {
+  const double r = 1.0;  // thickness 2 / 2
+  const int xa = (int)floor(fmin(q.x0, q.x1) - r), xb = (int)ceil(fmax(q.x0, q.x1) + r);
+  const int ya = (int)floor(fmin(q.y0, q.y1) - r), yb = (int)ceil(fmax(q.y0, q.y1) + r);
+  *x0 = max(xa, 0);
+  *y0 = max(ya, 0);
+  *bw = min(xb, W - 1) - *x0 + 1;
+  *bh = min(yb, H - 1) - *y0 + 1;
+  return *bw > 0 && *bh > 0;
+}
+__device__ __forceinline__ bool seg_covers(const DrawPrim& q, int x, int y) {
+  const double r = 1.0;
+  const double dx = q.x1 - q.x0, dy = q.y1 - q.y0, l2 = dx * dx + dy * dy;
+  double u = l2 > 0 ? ((x - q.x0) * dx + (y - q.y0) * dy) / l2 : 0.0;
+  u = fmin(1.0, fmax(0.0, u));
+  const double ex = q.x0 + u * dx - x, ey = q.y0 + u * dy - y;
+  return ex * ex + ey * ey <= r * r;
+}
+template <bool PAINT>
+__global__ __launch_bounds__(256) void k_draw(const DrawPrim* prims, uint32_t* last, uint8_t* bgr, int W, int H) {
+  const int p = blockIdx.x;
+  const DrawPrim q = prims[p];
+  int x0, y0, bw, bh;
+  if (!seg_box(q, W, H, &x0, &y0, &bw, &bh)) return;
+  for (int i = threadIdx.x; i < bw * bh; i += 256) {
+    const int x = x0 + i % bw, y = y0 + i / bw;
+    if (!seg_covers(q, x, y)) continue;
+    const size_t o = (size_t)y * W + x;
+    if (!PAINT) {
+      atomicMax(last + o, (uint32_t)(p + 1));
+    } else if (last[o] == (uint32_t)(p + 1)) {
+      bgr[3 * o + 0] = q.bgr[0];
+      bgr[3 * o + 1] = q.bgr[1];
+      bgr[3 * o + 2] = q.bgr[2];
+      last[o] = 0;
+    }
+  }
+}
+
+hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bgr, int W, int H, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_draw<false>, dim3(n), dim3(256), 0, st, prims, last, bgr, W, H);
+  hipLaunchKernelGGL(k_draw<true>, dim3(n), dim3(256), 0, st, prims, last, bgr, W, H);
+  return hipGetLastError();
+}
+
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt) {

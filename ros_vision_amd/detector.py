@@ -33,6 +33,7 @@ EXPORTS = [
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
     "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
+    "at_draw_outlines_device",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -185,6 +186,8 @@ def load_library(path: str = LIB_PATH):
         L.at_gp_copy.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
         L.at_gp_preprocess_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                               C.c_void_p]
+    if hasattr(L, "at_draw_outlines_device"):
+        L.at_draw_outlines_device.argtypes = [C.c_void_p, C.POINTER(AtDetection), C.c_int, C.c_void_p]
     _LIB = L
     return L
 
@@ -412,6 +415,15 @@ class GpuDetector:
     def detections(self, frame=0):
         """GpuDetector::Detections (apriltag_gpu.h:93), sorted by id."""
         return self._last[frame]
+
+    def draw_outlines_device(self, bgr_ptr: int, frame=0):
+        """at_draw_outlines_device: the annotated image of `frame` of the last batch
+        (outlines and ids, apriltag_utils.cu:54-79) drawn onto the device-resident
+        BGR8 image at `bgr_ptr` (width x height x 3)."""
+        n = min(self._n[frame], self._cap)
+        addr = C.addressof(self._out) + frame * self._cap * C.sizeof(AtDetection)
+        first = C.cast(C.c_void_p(addr), C.POINTER(AtDetection))
+        _check(load_library().at_draw_outlines_device(self._h, first, n, bgr_ptr), "at_draw_outlines_device")
 
     def frame_status(self, frame=0):
         return load_library().at_frame_status(self._h, frame)

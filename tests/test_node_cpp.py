@@ -197,3 +197,51 @@ def test_mock_node_matches_python_node_and_oracle(built, oracle_mod, tmp_path):
     assert proto.read_bytes() == bytes.fromhex(lines[-1]["proto_hex"])
     rows = csv.read_text().splitlines()
     assert rows[0].startswith("latency_us,det_time_us") and len(rows) == 3
+
+
+@pytest.mark.gpu
+def test_gpu_outlines_match_cpu_drawing(nodelib):
+    """at_draw_outlines_device draws the annotated image onto the
+    BGR frame in HBM pixel-identically to the node's CPU drawing -- on a stream
+    frame's real detections, and on hand-made overlapping ones (crossing sides,
+    ids over edges: the last primitive in drawing order wins, as on the CPU)."""
+    import torch
+    from ros_vision_amd import detector as D
+    from ros_vision_amd import synth
+    L = D.load_library()
+    W, H = 1280, 720
+    _, gray, _ = synth.stream_frame(W, H, 9)
+    bgr = np.ascontiguousarray(np.repeat(gray[:, :, None], 3, axis=2))
+    det = D.GpuDetector(W, H)
+    dets = det.detect(bgr, fmt=D.AT_FMT_BGR8)
+    assert len(dets) > 10
+    cpu = bgr.copy()
+    nodelib.at_node_draw_detection_outlines(cpu.ctypes.data, W, H, det._out, len(dets))
+    dev = torch.from_numpy(bgr).cuda()
+    det.draw_outlines_device(dev.data_ptr())
+    gpu_img = dev.cpu().numpy()
+    assert not np.array_equal(cpu, bgr)
+    assert np.array_equal(gpu_img, cpu), int((gpu_img != cpu).any(axis=-1).sum())
+    # overlapping hand-made detections, multi-digit ids, corners partly off-image
+    raw = (D.AtDetection * 4)()
+    quads = [[(10.5, 10.2), (200.7, 30.1), (180.3, 190.9), (20.2, 170.4)],
+             [(100.1, 50.8), (300.6, 60.2), (290.2, 230.7), (90.9, 220.3)],
+             [(-20.0, 100.0), (60.0, 80.0), (70.0, 260.0), (-30.0, 250.0)],
+             [(150.0, 100.0), (151.0, 100.5), (151.5, 101.0), (150.2, 101.2)]]
+    for i, q in enumerate(quads):
+        raw[i].id = [586, 12, 7, 100][i]
+        for k, (x, y) in enumerate(q):
+            raw[i].p[k][0], raw[i].p[k][1] = x, y
+        raw[i].c[0] = sum(x for x, _ in q) / 4
+        raw[i].c[1] = sum(y for _, y in q) / 4
+    small = D.GpuDetector(320, 240)
+    base = (np.arange(320 * 240 * 3) % 251).astype(np.uint8).reshape(240, 320, 3)
+    cpu = base.copy()
+    nodelib.at_node_draw_detection_outlines(cpu.ctypes.data, 320, 240, raw, 4)
+    dev = torch.from_numpy(base).cuda()
+    assert L.at_draw_outlines_device(small._h, raw, 4, dev.data_ptr()) == 0
+    assert np.array_equal(dev.cpu().numpy(), cpu)
+    # the scratch plane is left clear: drawing again on a fresh copy gives the same image
+    dev2 = torch.from_numpy(base).cuda()
+    assert L.at_draw_outlines_device(small._h, raw, 4, dev2.data_ptr()) == 0
+    assert np.array_equal(dev2.cpu().numpy(), cpu)
