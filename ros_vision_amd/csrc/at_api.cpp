@@ -386,7 +386,6 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.ht_rank = (uint32_t*)dalloc(B * kHashSlots * 4);
   b.ht_off = (uint32_t*)dalloc(B * kHashSlots * 4);
   b.ht_cur = (uint32_t*)dalloc(B * kHashSlots * 4);
-  b.plist = (uint64_t*)dalloc(B * kMaxPairs * 8);
   b.pair_cnt = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.pair_off = (uint32_t*)dalloc(B * kMaxPairs * 4);
   b.pair_sel = (uint32_t*)dalloc(B * kMaxPairs * 4);

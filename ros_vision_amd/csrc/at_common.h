@@ -196,7 +196,6 @@ struct DevBufs {
   uint32_t* ht_rank;  // [B][kHashSlots]
   uint32_t* ht_off;   // [B][kHashSlots]
   uint32_t* ht_cur;   // [B][kHashSlots]
-  uint64_t* plist;    // [B][kMaxPairs]   k_pairs' sort list of frames with more than 1024 pairs
   uint32_t* pair_cnt; // [B][kMaxPairs]
   uint32_t* pair_off; // [B][kMaxPairs]
   uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair

@@ -409,11 +409,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       if (bb == 0 && T(pr - 1, pc + 1) == 0) tR = s_par[slot_of<TWD>(bty - 1, btx, 2)];
     }
     // the left neighbour's targets (same wave: rows never straddle waves)
-    // (DPP wave_shr:1 moves: lane 0 / the first lane of a block row never uses them)
-    const uint32_t pUL = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tUL, 0x138, 0xf, 0xf, false);
-    const uint32_t pU = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tU, 0x138, 0xf, 0xf, false);
-    const uint32_t pUR = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tUR, 0x138, 0xf, 0xf, false);
-    const uint32_t pR = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone, (int)tR, 0x138, 0xf, 0xf, false);
+    const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
     __syncthreads();
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
@@ -609,39 +605,13 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   uint32_t* size = b.size + fo;
   const uint32_t n = b.nlroot[tl];
   const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-  // four local roots per lane at a time, their finds in lockstep (independent
-  // loads issued together) and each count loaded with the first parent
-  constexpr int kJ = 4;
-  for (uint32_t k0 = threadIdx.x; k0 < n; k0 += 64 * kJ) {
-    uint32_t l[kJ], p[kJ], c[kJ], r[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; j++) l[j] = k0 + 64 * j < n ? lr[k0 + 64 * j] : 0xffffffffu;
-#pragma unroll
-    for (int j = 0; j < kJ; j++) {
-      p[j] = l[j] != 0xffffffffu ? g_load(par + l[j]) : l[j];
-      c[j] = l[j] != 0xffffffffu ? size[l[j]] : 0u;
-      r[j] = l[j];
-    }
-    bool more = true;
-    while (more) {
-      more = false;
-#pragma unroll
-      for (int j = 0; j < kJ; j++) {
-        if (p[j] != r[j]) {
-          r[j] = p[j];
-          more = true;
-        }
-      }
-      if (!more) break;
-#pragma unroll
-      for (int j = 0; j < kJ; j++) p[j] = l[j] != 0xffffffffu ? g_load(par + r[j]) : r[j];
-    }
-#pragma unroll
-    for (int j = 0; j < kJ; j++) {
-      if (l[j] != 0xffffffffu && r[j] != l[j]) {
-        par[l[j]] = r[j];  // unions are over: a concurrent find sees the old parent or r, both lead to r
-        atomicAdd(size + r[j], c[j]);  // result unused: no round trip (size[l] is dead from here on)
-      }
+  for (uint32_t k = threadIdx.x; k < n; k += 64) {
+    const uint32_t l = lr[k];
+    const uint32_t r = g_find(par, l);
+    if (r != l) {
+      par[l] = r;  // unions are over: a concurrent find sees the old parent or r, both lead to r
+      const uint32_t cnt = size[l];
+      atomicAdd(size + r, cnt);  // result unused: no round trip (size[l] is dead from here on)
     }
   }
 }
@@ -659,18 +629,10 @@ __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
   const uint32_t* size = b.size + fo;
   const uint32_t n = b.nlroot[tl];
   const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-  constexpr int kJ = 4;  // four per lane at a time: three round trips for all of them
-  for (uint32_t k0 = threadIdx.x; k0 < n; k0 += 64 * kJ) {
-    uint32_t l[kJ], r[kJ], z[kJ];
-#pragma unroll
-    for (int j = 0; j < kJ; j++) l[j] = k0 + 64 * j < n ? lr[k0 + 64 * j] : 0xffffffffu;
-#pragma unroll
-    for (int j = 0; j < kJ; j++) r[j] = l[j] != 0xffffffffu ? par[l[j]] : 0u;
-#pragma unroll
-    for (int j = 0; j < kJ; j++) z[j] = l[j] != 0xffffffffu ? size[r[j]] : 0u;
-#pragma unroll
-    for (int j = 0; j < kJ; j++)
-      if (l[j] != 0xffffffffu) par[l[j]] = r[j] | (z[j] >= 25 ? kKeptBit : 0u);
+  for (uint32_t k = threadIdx.x; k < n; k += 64) {
+    const uint32_t l = lr[k];
+    const uint32_t r = par[l];
+    par[l] = r | (size[r] >= 25 ? kKeptBit : 0u);
   }
 }
 
@@ -759,7 +721,7 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
 template <bool KEPT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_boundary(DevBufs b, Geom g) {
+__global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
   // points staged in LDS up to kBndStage (typical tiles hold ~0.7 points per
@@ -849,10 +811,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       }
     }
     uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
-    // run heads of the four directions: their first hash probes are issued
-    // together (one LDS round trip instead of four); a key not at its home slot
-    // (first sighting in the tile, or a collision) takes the probing insert
-    uint32_t hl[4];  // run length at run heads, 0 elsewhere (keys: pk[dir] >> 24)
 #pragma unroll
     for (int dir = 0; dir < 4; dir++) {
       const bool has = pk[dir] != 0;
@@ -863,17 +821,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       const uint64_t prev = wave_shr1_u64(r01);
       const bool same = has && lane > 0 && prev == r01;
       const uint64_t same_mask = __ballot(same);
-      hl[dir] = has && !same ? run_len(same_mask, lane) : 0u;
-    }
-    uint64_t home[4];
-#pragma unroll
-    for (int dir = 0; dir < 4; dir++) home[dir] = hl[dir] ? s_pkey[mix_hash(pk[dir] >> 24) & (kLdsPairSlots - 1)] : 0ull;
-#pragma unroll
-    for (int dir = 0; dir < 4; dir++) {
-      if (!hl[dir]) continue;
-      const uint64_t r01 = pk[dir] >> 24;
-      if (home[dir] == r01) atomicAdd(s_pcnt + (mix_hash(r01) & (kLdsPairSlots - 1)), hl[dir]);
-      else if (!lds_pair_add(s_pkey, s_pcnt, r01, hl[dir])) bnd_spill(b, f, r01, hl[dir]);  // LDS table full
+      if (has && !same) {
+        const uint32_t len = run_len(same_mask, lane);
+        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) bnd_spill(b, f, r01, len);  // LDS table full
+      }
     }
     // wave-aggregated append of the points into the LDS staging buffer
     uint32_t wbase = 0;
@@ -957,14 +908,6 @@ constexpr int kGrpEnt = 128;  // tile entries with an LDS cursor in k_group (typ
 constexpr uint32_t kGrpDrop = 0xfffffffeu, kGrpFallback = 0xffffffffu;
 constexpr int kPairsEntCache = 4;  // entries per thread whose hash slot k_pairs keeps in registers
 
-// LDS: the frame's pair hash packs key (40 bits) and point count (24 bits) in one
-// word (32 KB); the sort list of a frame's <= 1024 pairs and its sorted runs take
-// 8 KB each; frames with more pairs sort their list in global memory (b.plist).
-// 45 KB per workgroup (was 84): a batch's k_pairs finds a CU sooner while other
-// batches' kernels fill the GPU.
-constexpr int kPairsLdsList = 1024;
-constexpr int kCntBits = 24;
-constexpr uint64_t kCntMask = (1ull << kCntBits) - 1;
 __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
@@ -972,29 +915,30 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     if (probe && f == 0 && tid == 0) b.probe[i] = wall_clock64();
   };
   stamp(0);
-  __shared__ uint64_t t_hash[kHashSlots];  // (key << 24) | count; 0 = empty
-  __shared__ uint64_t s_list[kPairsLdsList];
-  __shared__ uint64_t s_aux[kPairsLdsList];
+  __shared__ uint64_t t_key[kHashSlots];
+  __shared__ uint32_t t_cnt[kHashSlots];
+  __shared__ uint64_t s_list[kMaxPairs];
   __shared__ uint32_t s_n, s_full, s_np;
   __shared__ uint32_t s_wsum[16];
-  for (int i = tid; i < kHashSlots; i += 1024) t_hash[i] = 0;
+  for (int i = tid; i < kHashSlots; i += 1024) {
+    t_key[i] = 0;
+    t_cnt[i] = 0;
+  }
   if (tid == 0) { s_n = 0; s_full = 0; s_np = 0; }
   __syncthreads();
-  // merge the per-tile pair histograms of k_boundary in LDS (a frame's pairs hold
-  // fewer than 2^24 points each: the count never carries into the key)
+  // merge the per-tile pair histograms of k_boundary in LDS: wave w takes
+  // tiles w, w + 16, ...; then the overflow entries of crowded tiles
   auto merge = [&](uint64_t key, uint32_t cnt) -> uint32_t {
     uint32_t h = (uint32_t)mix_hash(key) & (kHashSlots - 1);
     for (int probe = 0; probe < kHashSlots; probe++) {
-      const uint64_t w = t_hash[h];
-      if (w != 0 && (w >> kCntBits) == key) {
-        atomicAdd((unsigned long long*)&t_hash[h], (unsigned long long)cnt);
+      const uint64_t k = t_key[h];
+      if (k == key) {
+        atomicAdd(&t_cnt[h], cnt);
         return h;
-      } else if (w == 0) {
-        const uint64_t prev =
-            atomicCAS((unsigned long long*)&t_hash[h], 0ull, (unsigned long long)((key << kCntBits) | cnt));
-        if (prev == 0) return h;
-        if ((prev >> kCntBits) == key) {
-          atomicAdd((unsigned long long*)&t_hash[h], (unsigned long long)cnt);
+      } else if (k == 0) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&t_key[h], 0ull, (unsigned long long)key);
+        if (prev == 0 || prev == key) {
+          atomicAdd(&t_cnt[h], cnt);
           return h;
         }
       }
@@ -1018,7 +962,6 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
     const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
     const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
-    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);  // (same round trip)
     const uint32_t incl_e = block_incl_scan(ne, s_wsum, &tot_e, 16);
     if (tid < ntb) s_tpre[tid] = incl_e - ne;
     if (tid == 0) s_tpre[ntb] = tot_e;
@@ -1043,6 +986,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
         b.pent_cnt[e] = kGrpFallback;  // beyond the register cache: k_group reserves per point
       }
     }
+    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
     for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
     __syncthreads();
     if (tid == 0) {
@@ -1052,14 +996,11 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   }
   __syncthreads();
   stamp(1);
-  uint64_t* glist = b.plist + (size_t)f * kMaxPairs;
   for (int s = tid; s < kHashSlots; s += 1024) {
-    const uint64_t w = t_hash[s];
-    if (w) {
+    const uint64_t k = t_key[s];
+    if (k) {
       const uint32_t i = atomicAdd(&s_n, 1u);
-      const uint64_t lk = ((w >> kCntBits) << kHashBits) | (uint64_t)s;
-      if (i < (uint32_t)kPairsLdsList) s_list[i] = lk;
-      else if (i < (uint32_t)kMaxPairs) glist[i] = lk;
+      if (i < kMaxPairs) s_list[i] = (k << kHashBits) | (uint64_t)s;
     }
   }
   __syncthreads();
@@ -1071,79 +1012,48 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   }
   // the lookup table used by k_group: keys of every slot (0 = empty)
   for (int s = tid; s < kHashSlots; s += 1024) {
-    const uint64_t w = t_hash[s];
-    b.ht_key[(size_t)f * kHashSlots + s] = w >> kCntBits;
-    b.ht_cnt[(size_t)f * kHashSlots + s] = (uint32_t)(w & kCntMask);
+    b.ht_key[(size_t)f * kHashSlots + s] = t_key[s];
+    b.ht_cnt[(size_t)f * kHashSlots + s] = t_cnt[s];
   }
   int np2 = 64;
   while (np2 < (int)n) np2 <<= 1;
-  const bool big = n > (uint32_t)kPairsLdsList;
-  uint64_t* list = big ? glist : s_list;
-  if (big) {
-    // more pairs than the LDS list holds (dense texture): the whole list in
-    // global memory (one workgroup's own scratch) and a bitonic sort there
-    for (int i = tid; i < kPairsLdsList; i += 1024) glist[i] = s_list[i];
-  }
-  for (int i = (int)n + tid; i < np2; i += 1024) list[i] = ~0ull;
+  for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
   __syncthreads();
   stamp(2);
-  if (!big) {
-    // keys are unique (the slot rides in the low bits).  Each wave sorts its 64
-    // keys in registers (bitonic, lane exchanges), writes the sorted run, and a
-    // key's rank is its position in its own run plus, for every other run, the
-    // number of smaller keys there (binary searches, all runs at once)
-    const int nw = (int)((n + 63) >> 6);
-    const int w = tid >> 6;
-    const uint32_t ln = lane_id();
-    uint64_t* run = s_aux;  // [nw][64] sorted runs (~0 padding past n)
-    const uint64_t key0 = s_list[tid];  // ~0 past n (filled above)
-    if (w < nw) {
-      uint64_t key = key0;
-#pragma unroll
-      for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          const uint64_t o = __shfl_xor(key, j);
-          const bool up = (ln & k) == 0, lower = (ln & j) == 0;
-          // keep the smaller of the pair in the lower lane of an ascending block
-          key = ((key < o) == (lower == up)) ? key : o;
-        }
-      }
-      run[w * 64 + ln] = key;
+  if (n <= 1024) {
+    // rank sort (keys are unique: the slot rides in the low bits); t_key is free
+    // once the lookup table has been written out above.  P = 1024 / n threads per
+    // key, each counting the smaller keys of a 1/P slice of the list (a frame's
+    // ~400 pairs: 2 threads per key, half the serial LDS reads)
+    const int P = (int)(1024 / (n ? n : 1u));
+    uint32_t* s_rank = reinterpret_cast<uint32_t*>(t_key + 2048);
+    if (tid < (int)n) s_rank[tid] = 0;
+    __syncthreads();
+    if (tid < P * (int)n) {
+      const int i = tid % (int)n, h = tid / (int)n;
+      const uint64_t key = s_list[i];
+      const int j1 = (int)(((uint32_t)h + 1) * n / (uint32_t)P);
+      int j = (int)((uint32_t)h * n / (uint32_t)P);
+      uint32_t r = 0;
+      for (; j + 4 <= j1; j += 4)
+        r += (s_list[j] < key) + (s_list[j + 1] < key) + (s_list[j + 2] < key) + (s_list[j + 3] < key);
+      for (; j < j1; j++) r += s_list[j] < key;
+      if (r) atomicAdd(&s_rank[i], r);
     }
     __syncthreads();
-    if (tid < (int)n) {
-      uint32_t r = 0;
-      uint32_t pos[16];
-#pragma unroll
-      for (int v = 0; v < 16; v++) pos[v] = 0;
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1) {
-#pragma unroll
-        for (int v = 0; v < 16; v++)
-          if (v < nw && run[v * 64 + pos[v] + step - 1] < key0) pos[v] += step;
-      }
-#pragma unroll
-      for (int v = 0; v < 16; v++)
-        if (v < nw) r += pos[v] + (run[v * 64 + pos[v]] < key0 ? 1u : 0u);
-      // (in its own run the key itself is not counted: equal, not smaller)
-      s_list[r] = key0;  // every key was read before the barrier above
-    }
+    if (tid < (int)n) t_key[s_rank[tid]] = s_list[tid];
+    __syncthreads();
+    if (tid < (int)n) s_list[tid] = t_key[tid];
     __syncthreads();
   } else {
-    block_bitonic_sort<uint64_t, 1024>(glist, np2);
+    block_bitonic_sort<uint64_t, 1024>(s_list, np2);
   }
   stamp(3);
   // counts in rank order (straight from the hash slots), exclusive scan -> offsets;
   // each thread owns 4 consecutive ranks
   const int i0 = tid * 4;
-  auto cnt_at = [&](int i) -> uint32_t {
-    return i < (int)n ? (uint32_t)(t_hash[list[i] & (kHashSlots - 1)] & kCntMask) : 0u;
-  };
+  auto cnt_at = [&](int i) -> uint32_t { return i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u; };
   const uint32_t c0 = cnt_at(i0), c1 = cnt_at(i0 + 1), c2 = cnt_at(i0 + 2), c3 = cnt_at(i0 + 3);
-  uint32_t sl[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) sl[k] = i0 + k < (int)n ? (uint32_t)(list[i0 + k] & (kHashSlots - 1)) : 0u;
   const uint32_t tsum = c0 + c1 + c2 + c3;
   const uint32_t incl = wave_incl_scan(tsum, AddOp(), 0u);
   const uint32_t lane = lane_id();
@@ -1158,7 +1068,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   // work-list appends by size class: LDS slots, then one global atomic per
   // class per workgroup
   __shared__ uint32_t s_ccnt[kNumCls], s_cbase[kNumCls];
-  __syncthreads();  // s_n / s_full / s_wsum / t_hash reads done
+  __syncthreads();  // s_n / s_full / s_wsum reads done
   if (tid < kNumCls) s_ccnt[tid] = 0;
   __syncthreads();
   int cls[4];
@@ -1175,17 +1085,11 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __syncthreads();
   if (tid < kNumCls) s_cbase[tid] = s_ccnt[tid] ? atomicAdd(b.ncls + tid, s_ccnt[tid]) : 0u;
   __syncthreads();
-  // segment bases of the tiles' first kGrpEnt entries: per pair slot its segment
-  // offset (kGrpDrop outside the size bounds) and an LDS cursor, over the hash
-  // table (every read of it is done); the cursors' final values seed k_group's
-  // per-point reservations
-  uint32_t* t_off = reinterpret_cast<uint32_t*>(t_hash);
-  uint32_t* t_cur = t_off + kHashSlots;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
     if (i < (int)n) {
-      const uint32_t slot = sl[k];
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
       b.ht_rank[(size_t)f * kHashSlots + slot] = (uint32_t)i;
       b.ht_off[(size_t)f * kHashSlots + slot] = offs[k];
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
@@ -1193,7 +1097,19 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       b.pair_sel[(size_t)f * kMaxPairs + i] = 0;
       if (cls[k] >= 0)
         b.work[(size_t)cls[k] * b.wcap + s_cbase[cls[k]] + lslot[k]] = ((uint32_t)f << 16) | (uint32_t)i;
-      t_off[slot] = cs[k] >= g.min_cluster && cs[k] <= g.max_cluster ? offs[k] : kGrpDrop;
+    }
+  }
+  // segment bases of the tiles' first kGrpEnt entries (LDS cursors per pair slot;
+  // t_key's storage is free since the sort), then the cursors' final values seed
+  // k_group's per-point reservations
+  uint32_t* t_off = reinterpret_cast<uint32_t*>(t_key);
+  uint32_t* t_cur = t_off + kHashSlots;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + k;
+    if (i < (int)n) {
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      t_off[slot] = offs[k];
       t_cur[slot] = 0;
     }
   }
@@ -1201,15 +1117,19 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 #pragma unroll
   for (int k = 0; k < kPairsEntCache; k++) {
     if (c_slot[k] != 0xffffffffu && c_lds[k]) {
-      const uint32_t o = t_off[c_slot[k]];
-      b.pent_cnt[c_idx[k]] = o != kGrpDrop ? o + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
+      const uint32_t tc = t_cnt[c_slot[k]];
+      const bool keep = tc >= g.min_cluster && tc <= g.max_cluster;
+      b.pent_cnt[c_idx[k]] = keep ? t_off[c_slot[k]] + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
-    if (i < (int)n) b.ht_cur[(size_t)f * kHashSlots + sl[k]] = t_cur[sl[k]];
+    if (i < (int)n) {
+      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      b.ht_cur[(size_t)f * kHashSlots + slot] = t_cur[slot];
+    }
   }
   stamp(5);
 }
@@ -3087,9 +3007,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
   __syncthreads();
   const uint32_t nq = qpre[B];
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[128 + k], counts [160 + k])
-  // (in LDS rather than 21 registers per lane)
-  __shared__ uint32_t pacc[21];
-  if (tid < 21) pacc[tid] = 0;
+  uint32_t pacc[21] = {0};
   uint64_t t_last = 0;
   auto phase = [&](int k) {
     if (prm.probe && tid == 0) {
@@ -3422,28 +3340,28 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
     }
-    const float margin = (float)margin_d;
-    if (margin >= 0 && bc != 0xffffffffu) {  // uniform (bc is the wave minimum)
-      const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
-      DevDetection d;
-      d.id = b.book_id[ent];
-      d.hamming = hd;
-      d.decision_margin = margin;
-      d.blob_rank = (int32_t)qrank;
-      const double R[9] = {c_rot_c[rot], -c_rot_s[rot], 0, c_rot_s[rot], c_rot_c[rot], 0, 0, 0, 1};
-      for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-          double acc = 0;
-          for (int k = 0; k < 3; k++) acc += S.H[i * 3 + k] * R[k * 3 + j];
-          d.H[i * 3 + j] = acc;
+    if (tid == 0) {
+      const float margin = (float)margin_d;
+      if (margin >= 0 && bc != 0xffffffffu) {
+        const int rot = bc >> 24, hd = (bc >> 16) & 0xff, ent = bc & 0xffff;
+        DevDetection d;
+        d.id = b.book_id[ent];
+        d.hamming = hd;
+        d.decision_margin = margin;
+        d.blob_rank = (int32_t)qrank;
+        const double R[9] = {c_rot_c[rot], -c_rot_s[rot], 0, c_rot_s[rot], c_rot_c[rot], 0, 0, 0, 1};
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += S.H[i * 3 + k] * R[k * 3 + j];
+            d.H[i * 3 + j] = acc;
+          }
+        hproject(d.H, 0, 0, &d.c[0], &d.c[1]);
+        for (int i = 0; i < 4; i++) {
+          const int tcx = (i == 1 || i == 2) ? 1 : -1;
+          const int tcy = (i < 2) ? 1 : -1;
+          hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
         }
-      hproject(d.H, 0, 0, &d.c[0], &d.c[1]);
-      for (int i = 0; i < 4; i++) {
-        const int tcx = (i == 1 || i == 2) ? 1 : -1;
-        const int tcy = (i < 2) ? 1 : -1;
-        hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
-      }
-      if (tid == 0) {
         const uint32_t di = atomicAdd(b.ndets + f, 1u);
         if (di < (uint32_t)kMaxDets) {
           b.dets[(size_t)f * kMaxDets + di] = d;
