@@ -106,15 +106,8 @@ def pmc_traffic(W, H):
 
 
 def render_pool(args, rank):
-    from ros_vision_amd import synth
-    codes = dict(__import__("ros_vision_amd").family_entries())
-    frames = np.empty((args.pool, args.height, 2 * args.width), np.uint8)
-    for i in range(args.pool):
-        f = rank * args.pool + i  # config C2 frame f: seed 766000 + f, ids 10f .. 10f+14 mod 587
-        gray, _ = synth.render_board(args.width, args.height, seed=766000 + f, ntags=args.tags,
-                                     ids=synth.stream_ids(f, args.tags, len(codes)), codes=codes)
-        frames[i] = synth.to_yuyv(gray)
-    return frames
+    from ros_vision_amd.stream import stream_pool
+    return stream_pool(args.width, args.height, args.pool, args.tags, rank)
 
 
 def host_cpus():
@@ -190,6 +183,7 @@ def main():
 
     import ros_vision_amd as rva
     from ros_vision_amd import multigpu
+    from ros_vision_amd.stream import StreamRunner
     W, H, B = args.width, args.height, args.batch
     assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
     scatter = args.ingest == "scatter"
@@ -231,29 +225,17 @@ def main():
         copied[id(d)].record()
         gwork[i] = dist.gather(send[i], gather_list=recv[i], dst=0, async_op=True)
 
+    runner = StreamRunner(dets, base, stride, npool, B)
+
     def batch_ptr(step):
-        off = (step * B) % npool
-        if off + B > npool:
-            off = 0
-        return base + off * stride
+        return base + runner.offset(step) * stride
 
     def run(nsteps, step0=0):
-        """Round-robin over the detector instances: enqueue k, collect k-(instances-1)."""
+        """Round-robin over the detector instances: enqueue k, collect k-(instances-1)
+        (ros_vision_amd/stream.py; tests/test_stream_parity.py checks this loop's output)."""
         if scatter:
             return run_scatter(nsteps, step0)
-        ndet = 0
-        prev = None
-        ni = len(dets)
-        inflight = []
-        for s in range(nsteps):
-            d = dets[s % ni]
-            d.enqueue_device(batch_ptr(step0 + s), stride, B)
-            inflight.append(d)
-            if len(inflight) == ni:
-                ndet += sum(inflight.pop(0).collect(counts_only=True))
-        for d in inflight:
-            ndet += sum(d.collect(counts_only=True))
-        return ndet
+        return runner.run(nsteps, step0)
 
     def run_scatter(nsteps, step0):
         """Scatter of step k+1 overlaps detection of step k (double-buffered)."""

@@ -375,6 +375,11 @@ class GpuDetector:
             return [self._n[f] for f in range(self._pending)]
         return self._unpack(self._pending)
 
+    def results(self):
+        """Detections of every frame of the last collected batch (after
+        collect(counts_only=True), builds the Python objects from the buffer)."""
+        return self._unpack(self._pending)
+
     # ---- per-stage timing (the reference's CudaEvent stage timers,
     #      apriltag_gpu.cu:1118-1163) ----------------------------------------
     def set_profiling(self, enable=True):

@@ -55,3 +55,48 @@ def compare_detections(gd, od, tol=1e-4):
             if not np.array_equal(np.floor(x), np.floor(y)) and nm != "H":
                 bad.append("integer %s id %d differ" % (nm, a.id))
     return bad
+
+
+# ---- goldens of the bench's own workloads (tools/make_stream_golden.py) --------
+
+def load_stream_golden(name):
+    """tests/golden/stream_<name>.npz as a dict of arrays, plus per-frame slices."""
+    import os
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "stream_%s.npz" % name)))
+    starts = np.concatenate([[0], np.cumsum(g["ndet"])])
+    g["_start"] = starts
+    return g
+
+
+def compare_with_stream_golden(g, f, dets, poses=None, tol=1e-4):
+    """Detections (and poses) of golden frame f: ids / hamming exact, integer parts of
+    c and p equal, margin / H / c / p (and pose R, t) within tol.  Poses whose two
+    minima have equal error are skipped (either is estimate_tag_pose's answer)."""
+    bad = []
+    a, b = int(g["_start"][f]), int(g["_start"][f + 1])
+    ids = [int(v) for v in g["det_id"][a:b]]
+    if [d.id for d in dets] != ids:
+        return ["frame %d ids differ: %s vs %s" % (f, [d.id for d in dets], ids)]
+    for k, d in enumerate(dets):
+        i = a + k
+        if d.hamming != int(g["det_hamming"][i]):
+            bad.append("frame %d id %d hamming" % (f, d.id))
+        if abs(d.decision_margin - float(g["det_margin"][i])) > tol:
+            bad.append("frame %d id %d margin %r vs %r" % (f, d.id, d.decision_margin, float(g["det_margin"][i])))
+        for nm, x, y in (("H", d.H.ravel(), g["det_H"][i]), ("c", d.c, g["det_c"][i]),
+                         ("p", d.p.ravel(), g["det_p"][i])):
+            if not np.allclose(x, y, rtol=0, atol=tol):
+                bad.append("frame %d id %d %s max diff %g" % (f, d.id, nm, float(np.max(np.abs(x - y)))))
+            if nm != "H" and not np.array_equal(np.floor(x), np.floor(y)):
+                bad.append("frame %d id %d integer %s differ" % (f, d.id, nm))
+    if poses is not None:
+        if [p.id for p in poses] != ids:
+            return bad + ["frame %d pose ids differ" % f]
+        for k, p in enumerate(poses):
+            i = a + k
+            e1, e2 = float(g["det_e1"][i]), float(g["det_e2"][i])
+            if abs(e1 - e2) <= 1e-9 * max(e1, e2, 1e-30):
+                continue
+            if (np.abs(p.R.ravel() - g["det_R"][i]).max() > tol or np.abs(p.t - g["det_t"][i]).max() > tol):
+                bad.append("frame %d id %d pose differs" % (f, p.id))
+    return bad

@@ -1,0 +1,98 @@
+"""GPU parity of the exact configurations the bench reports.
+
+* C2 headline: bench.py's own loop (ros_vision_amd.stream.StreamRunner) with
+  its defaults -- 4 detector instances x max_batch 128, enqueue_device / collect
+  round-robin over the 64-frame C2 pool replicated 4x in HBM, hipGraph replay,
+  then again with the live kernel timer (the split graphs of the timed region).
+  Every frame of every batch is compared with the committed oracle goldens.
+* C4 geometry in throughput mode: 8 1920x1080 frames, max_batch 8 (the
+  throughput-mode kernels), stage-by-stage against the live oracle and against
+  the goldens.
+
+Reference test this mirrors: test/gpu_detector_test.cu:122-157 (CpuAndGpuEqual),
+tightened to bit-exact ids / integer corners and 1e-4 on floats.
+"""
+import numpy as np
+import pytest
+
+from parity_util import compare_detections, compare_frame, compare_with_stream_golden, load_stream_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c2():
+    import make_stream_golden as mg
+    g = load_stream_golden("c2")
+    frames = mg.c2_frames(dict(__import__("ros_vision_amd").family_entries()))
+    assert [mg.digest(f) for f in frames] == list(g["frame_digest"]), "C2 pool renders differently"
+    return g, frames
+
+
+def test_bench_headline_configuration(c2):
+    import torch
+
+    import ros_vision_amd as rva
+    from ros_vision_amd.stream import StreamRunner
+    g, frames = c2
+    instances, B, copies = 4, 128, 4  # bench.py defaults
+    pool = frames.shape[0]
+    d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
+    stride = frames[0].nbytes
+    dets = [rva.GpuDetector(1280, 720, max_batch=B) for _ in range(instances)]
+    runner = StreamRunner(dets, d_frames.data_ptr(), stride, pool * copies, B)
+    seen = {"frames": 0, "dets": 0}
+    bad = []
+
+    def check(det, step, off):
+        res = det.results()
+        for j in range(B):
+            f = (off + j) % pool
+            assert det.frame_status(j) == 0
+            bad.extend(compare_with_stream_golden(g, f, res[j], det.poses(j)))
+            seen["dets"] += len(res[j])
+        seen["frames"] += B
+
+    n = runner.run(8, 0, on_batch=check)
+    assert bad == [], bad[:10]
+    assert seen["frames"] == 8 * B and n == seen["dets"] == 8 * B * 15
+    # the timed region of the bench: the kernel timer splits the graph around its kernel
+    for d in dets:
+        d.set_kernel_timer("k_blob_small")
+    runner.run(4, 8, on_batch=check)
+    assert bad == [], bad[:10]
+    ms = [d.kernel_time() for d in dets]
+    assert all(k > 0 and launches == 1 for k, launches in ms)
+    for d in dets:
+        d.set_kernel_timer(None)
+    # intermediate planes of each instance's last batch: threshold + labels bit-exact
+    import make_stream_golden as mg
+    for d in dets[:2]:
+        off = runner.offset(8 + dets.index(d))
+        for j in (0, 1, B - 1):
+            f = (off + j) % pool
+            assert mg.digest(d.copy_thresholded(j)) == g["thr_digest"][f]
+            assert mg.digest(d.copy_union_markers(j)) == g["labels_digest"][f]
+            assert d.num_pairs(j) == g["num_pairs"][f]
+
+
+def test_c4_1080p_throughput_mode(oracle_mod):
+    """1920x1080, 24 tags, max_batch 8 (throughput-mode kernels: 64-wide CCL tiles,
+    k_ccl_keep + k_boundary<true>, k_extents for every candidate, 256-thread
+    large-blob teams), frames resident in HBM."""
+    import torch
+
+    import make_stream_golden as mg
+    import ros_vision_amd as rva
+    g = load_stream_golden("c4")
+    frames = mg.c4_frames(dict(rva.family_entries()))
+    assert [mg.digest(f) for f in frames] == list(g["frame_digest"])
+    t = torch.from_numpy(frames).cuda()
+    det = rva.GpuDetector(1920, 1080, max_batch=8, debug_taps=True)
+    res = det.detect_device(t.data_ptr(), frames[0].nbytes, 8)
+    for f in range(8):
+        assert compare_with_stream_golden(g, f, res[f], det.poses(f)) == []
+        orc = oracle_mod.Oracle(1920, 1080)
+        orc.detect(frames[f], 0)
+        assert compare_frame(det, orc, frame_idx=f) == []
+        assert compare_detections(res[f], orc.detections()) == []
