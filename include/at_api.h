@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define AT_ABI_VERSION 3
+#define AT_ABI_VERSION 4
 
 enum {
   AT_OK = 0,
@@ -187,6 +187,15 @@ typedef struct {
 } at_pose;
 int at_poses(at_detector *d, int frame, at_pose *out, int cap);
 
+/* Detections of frame `frame` of the last collected batch again (the same records
+ * at_collect wrote, id order), e.g. when its cap_per_frame was smaller than the
+ * count it reported.  Returns the count or < 0. */
+int at_detections(at_detector *d, int frame, at_detection *out, int cap);
+/* Most detections one frame can yield (candidates before reconcile; the reference
+ * keeps every detection, apriltag_detect.cu:618-663): a cap_per_frame this large
+ * never truncates. */
+int at_max_detections(void);
+
 /* The node's per-frame tail over those poses (apriltags_cuda_detector.cu:425-462,
  * 595-599): robot = R_ext * t + t_ext (transformCameraToRobot), distance = |t|
  * in the camera frame, records sorted by ascending distance (stable).  Host
@@ -227,6 +236,13 @@ int at_gp_preprocess_device(const uint8_t *bgr, int width, int height, float *ou
  * Hershey font).  `dets` as at_collect returned them (host memory).  Runs on the
  * detector's stream and returns when the image is drawn. */
 int at_draw_outlines_device(at_detector *d, const at_detection *dets, int n, uint8_t *bgr);
+
+/* The node's published image for a host-fed BGR8 frame without a host copy and
+ * redraw: draws those outlines onto frame `frame` of the last batch where
+ * at_detect / at_detect_batch staged it in HBM, and copies the annotated image
+ * (width x height x 3) to `bgr_out` in host memory.  AT_E_INVALID unless the last
+ * batch was host BGR8 frames.  The staged copy is consumed (overwritten). */
+int at_annotate_staged(at_detector *d, int frame, const at_detection *dets, int n, uint8_t *bgr_out);
 
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);

@@ -7,9 +7,15 @@
 // frame; --proto-out / --image-out write the ApriltagListProto bytes and the
 // outlined bgr8 image of the last frame.
 //
-// usage: at_mock_node --width W --height H --format bgr8|yuyv|gray --frames F
-//        [--count N] [--calibration-dir D --camera-serial S] [--system-config C]
+// usage: at_mock_node --camera-serial S --format bgr8|yuyv|gray --frames F [--count N]
+//        [--vision-config-dir D] [--pin-to-core C --priority P]
 //        [--measurement-csv PATH] [--proto-out P] [--image-out I] [--device K]
+//   As the reference node (apriltags_cuda_detector.cu:137-193): the frame size, the
+//   intrinsics and the extrinsics come from the camera serial's records in the
+//   vision_config_data share directory, found through $AMENT_PREFIX_PATH
+//   (ament_index) or given with --vision-config-dir.  Without a serial's records
+//   (test setups) --width W --height H [--calibration-dir D] [--system-config C]
+//   give them directly (calibration default: the reference test camera).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -38,8 +44,8 @@ void on_camera(void* ctx, const std::vector<at_node::TagDetectionMsg>& v) { ((Si
 }  // namespace
 
 int main(int argc, char** argv) {
-  int W = 0, H = 0, count = -1, device = 0;
-  std::string fmt_s = "yuyv", frames_path, calib_dir, serial = "N/A", sys_cfg, csv, proto_out, image_out;
+  int W = 0, H = 0, count = -1, device = 0, pin = -1, priority = 80;
+  std::string fmt_s = "yuyv", frames_path, calib_dir, serial = "N/A", sys_cfg, csv, proto_out, image_out, share_dir;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
     if (k == "--width") W = std::atoi(v.c_str());
@@ -54,37 +60,58 @@ int main(int argc, char** argv) {
     else if (k == "--proto-out") proto_out = v;
     else if (k == "--image-out") image_out = v;
     else if (k == "--device") device = std::atoi(v.c_str());
+    else if (k == "--vision-config-dir") share_dir = v;
+    else if (k == "--pin-to-core") pin = std::atoi(v.c_str());
+    else if (k == "--priority") priority = std::atoi(v.c_str());
     else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
   }
+  at_node::Params prm;
+  prm.camera_serial = serial;
+  prm.measurement_mode = !csv.empty();
+  prm.timing_csv_path = csv;
+  prm.pin_to_core = pin;
+  prm.priority = priority;
+  // the reference test camera (test/gpu_detector_test.cu:62-73) unless a calibration is given
+  at_node::NodeConfig nc;
+  nc.cam = at_camera{905.495617, 907.909470, 609.916016, 352.682645, 0.059238, -0.075154, -0.003801, 0.001113, 0.0};
+  std::string err;
+  if (W <= 0 && H <= 0) {  // the node's set-up: everything from the serial's records
+    if (!at_node::resolve_node_config(serial, share_dir, &nc, &err)) {
+      std::fprintf(stderr, "config: %s\n", err.c_str());
+      return 1;
+    }
+  } else {
+    nc.camera.width = W;
+    nc.camera.height = H;
+    if (!calib_dir.empty() && !at_node::load_camera_calibration(calib_dir, serial, &nc.cam, &err)) {
+      std::fprintf(stderr, "calibration: %s\n", err.c_str());
+      return 1;
+    }
+    at_node::load_extrinsics(sys_cfg.empty() ? "/nonexistent" : sys_cfg, serial, nc.R, nc.t, &nc.location);
+  }
+  W = nc.camera.width;
+  H = nc.camera.height;
+  const std::string& location = nc.location;
   const at_pixfmt fmt = fmt_s == "bgr8" ? AT_FMT_BGR8 : (fmt_s == "gray" ? AT_FMT_GRAY8 : AT_FMT_YUYV);
   const size_t fb = (size_t)W * H * (fmt == AT_FMT_BGR8 ? 3 : (fmt == AT_FMT_YUYV ? 2 : 1));
   if (W <= 0 || H <= 0 || frames_path.empty()) {
-    std::fprintf(stderr, "usage: %s --width W --height H --format bgr8|yuyv|gray --frames FILE ...\n", argv[0]);
+    std::fprintf(stderr, "usage: %s --camera-serial S --format bgr8|yuyv|gray --frames FILE ...\n", argv[0]);
     return 2;
   }
   std::ifstream in(frames_path, std::ios::binary);
   std::vector<uint8_t> all((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
   const int nframes = (int)(all.size() / fb);
   if (count < 0 || count > nframes) count = nframes;
-
-  at_node::Params prm;
-  prm.camera_serial = serial;
-  prm.measurement_mode = !csv.empty();
-  prm.timing_csv_path = csv;
-  // the reference test camera (test/gpu_detector_test.cu:62-73) unless a calibration is given
-  at_camera cam{905.495617, 907.909470, 609.916016, 352.682645, 0.059238, -0.075154, -0.003801, 0.001113, 0.0};
-  std::string err;
-  if (!calib_dir.empty() && !at_node::load_camera_calibration(calib_dir, serial, &cam, &err)) {
-    std::fprintf(stderr, "calibration: %s\n", err.c_str());
-    return 1;
-  }
-  double R[9], t[3];
-  std::string location;
-  if (!sys_cfg.empty()) at_node::load_extrinsics(sys_cfg, serial, R, t, &location);
-  else at_node::load_extrinsics("/nonexistent", serial, R, t, &location);  // identity / zero
+  // applyCpuPinningAndScheduling (:601-605): failures are logged, not fatal
+  std::string sched_log;
+  const bool sched_ok = at_node::apply_cpu_pinning_and_scheduling(prm.pin_to_core, prm.priority, &sched_log);
+  std::fprintf(stderr, "%s", sched_log.c_str());
+  std::printf("{\"width\":%d,\"height\":%d,\"fx\":%.17g,\"location\":\"%s\",\"scheduling_applied\":%s,"
+              "\"networktables\":\"%s\"}\n",
+              W, H, nc.cam.fx, location.c_str(), sched_ok ? "true" : "false", nc.networktables.table_address.c_str());
   Sink sink;
   try {
-    at_node::DetectorCore core(W, H, prm, cam, R, t, device);
+    at_node::DetectorCore core(prm, nc, device);
     core.publish_robot = on_robot;
     core.publish_camera = on_camera;
     core.ctx = &sink;

@@ -1,9 +1,14 @@
 // at_node.cpp -- see at_node.h.  Host C++ only (the GPU work is behind at_api.h).
 #include "at_node.h"
 
+#include <pthread.h>
+#include <sched.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <fstream>
@@ -22,6 +27,7 @@ namespace {
 struct Json {
   enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
   double num = 0;
+  bool is_int = false;  // numeric literal without fraction or exponent (nlohmann is_number_integer)
   bool b = false;
   std::string str;
   std::vector<Json> arr;
@@ -110,6 +116,9 @@ struct Parser {
       v.num = strtod(p, &end);
       if (end == p) ok = false;
       v.kind = Json::Num;
+      v.is_int = end != p && std::find_if(p, (const char*)end, [](char c) {
+                               return c == '.' || c == 'e' || c == 'E';
+                             }) == (const char*)end;
       p = end;
     }
     return v;
@@ -197,6 +206,133 @@ bool load_extrinsics(const std::string& path, const std::string& serial, double 
   std::copy(Rt, Rt + 9, R);
   std::copy(tt, tt + 3, t);
   return true;
+}
+
+std::string package_share_directory(const std::string& package) {
+  const char* env = std::getenv("AMENT_PREFIX_PATH");
+  if (!env) return "";
+  std::stringstream ss(env);
+  std::string prefix;
+  while (std::getline(ss, prefix, ':')) {
+    if (prefix.empty()) continue;
+    const std::string marker = prefix + "/share/ament_index/resource_index/packages/" + package;
+    if (access(marker.c_str(), F_OK) == 0) return prefix + "/share/" + package;
+  }
+  return "";
+}
+
+bool load_camera_config(const std::string& path, const std::string& serial, CameraConfig* out) {
+  Json j;
+  if (!parse_file(path, &j, nullptr)) return false;
+  const Json* cmp = j.get("camera_mounted_positions");
+  const Json* c = cmp ? cmp->get(serial) : nullptr;
+  if (!c || c->kind != Json::Obj) return false;
+  auto str = [&](const char* k, std::string* v) {
+    const Json* e = c->get(k);
+    if (!e || e->kind != Json::Str) return false;
+    *v = e->str;
+    return true;
+  };
+  auto integer = [&](const char* k, int* v) {
+    const Json* e = c->get(k);
+    if (!e || e->kind != Json::Num || !e->is_int) return false;
+    *v = (int)e->num;
+    return true;
+  };
+  CameraConfig cfg;
+  if (!str("location", &cfg.location) || !str("format", &cfg.format) || !integer("height", &cfg.height) ||
+      !integer("width", &cfg.width) || !integer("frame_rate", &cfg.frame_rate) ||
+      !str("api_preference", &cfg.api_preference))
+    return false;  // incomplete records are skipped (config_loader.cpp:83-94)
+  *out = cfg;
+  return true;
+}
+
+NetworkTablesConfig load_network_tables_config(const std::string& path) {
+  NetworkTablesConfig nt;
+  Json j;
+  if (!parse_file(path, &j, nullptr)) return nt;
+  const Json* c = j.get("network_tables_config");
+  if (const Json* a = c ? c->get("table_address") : nullptr)
+    if (a->kind == Json::Str) nt.table_address = a->str;
+  if (const Json* n = c ? c->get("table_name") : nullptr)
+    if (n->kind == Json::Str) nt.table_name = n->str;
+  return nt;
+}
+
+bool resolve_node_config(const std::string& serial, const std::string& share_dir, NodeConfig* out, std::string* err) {
+  NodeConfig& nc = *out;
+  nc = NodeConfig{};
+  nc.share_dir = share_dir.empty() ? package_share_directory("vision_config_data") : share_dir;
+  if (nc.share_dir.empty()) {
+    if (err) *err = "package vision_config_data not found (AMENT_PREFIX_PATH) and no config directory given";
+    return false;
+  }
+  nc.system_config = nc.share_dir + "/data/system_config.json";
+  nc.calibration_dir = nc.share_dir + "/data/calibration";
+  if (!load_camera_calibration(nc.calibration_dir, serial, &nc.cam, err)) return false;
+  nc.have_extrinsics = load_extrinsics(nc.system_config, serial, nc.R, nc.t, &nc.location);
+  nc.networktables = load_network_tables_config(nc.system_config);
+  if (!load_camera_config(nc.system_config, serial, &nc.camera)) {  // apriltags_cuda_detector.cu:159-169
+    if (err) *err = "Failed to load camera configuration for serial: " + serial;
+    return false;
+  }
+  return true;
+}
+
+bool apply_cpu_pinning_and_scheduling(int pin_to_core, int priority, std::string* log) {
+  auto say = [&](const std::string& m) {
+    if (log) *log += m + "\n";
+  };
+  if (pin_to_core == -1) {
+    say("CPU pinning disabled (pin_to_core = -1)");
+    return true;
+  }
+  bool ok = true;
+  const int ncores = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (pin_to_core < 0 || pin_to_core >= ncores) {
+    say("Invalid CPU core " + std::to_string(pin_to_core) + ". System has " + std::to_string(ncores) + " cores");
+    ok = false;
+  } else {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(pin_to_core, &set);
+    const int r = pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    if (r) {
+      say(std::string("Failed to set CPU affinity: ") + std::strerror(r));
+      ok = false;
+    } else {
+      say("Pinned to CPU core " + std::to_string(pin_to_core));
+    }
+  }
+  const int lo = sched_get_priority_min(SCHED_FIFO), hi = sched_get_priority_max(SCHED_FIFO);
+  if (priority < lo || priority > hi) {
+    say("Invalid priority " + std::to_string(priority) + " for SCHED_FIFO");
+    ok = false;
+  } else {
+    sched_param sp{};
+    sp.sched_priority = priority;
+    const int r = pthread_setschedparam(pthread_self(), SCHED_FIFO, &sp);
+    if (r) {
+      say(std::string("Failed to set real-time scheduling: ") + std::strerror(r) +
+          " (needs root or CAP_SYS_NICE)");
+      ok = false;
+    } else {
+      say("SCHED_FIFO priority " + std::to_string(priority));
+    }
+  }
+  if (ok) {  // verifySettings (:124-171)
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    int policy = 0;
+    sched_param sp{};
+    if (pthread_getaffinity_np(pthread_self(), sizeof(set), &set) || !CPU_ISSET(pin_to_core, &set) ||
+        pthread_getschedparam(pthread_self(), &policy, &sp) || policy != SCHED_FIFO || sp.sched_priority != priority) {
+      say("verification of affinity / scheduling failed");
+      ok = false;
+    }
+  }
+  return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -312,13 +448,24 @@ DetectorCore::DetectorCore(int width, int height, const Params& params, const at
     : width_(width), height_(height), params_(params) {
   for (int i = 0; i < 9; ++i) R_[i] = extr_R ? extr_R[i] : ((i % 4 == 0) ? 1.0 : 0.0);
   for (int i = 0; i < 3; ++i) t_[i] = extr_t ? extr_t[i] : 0.0;
+  init(cam, device);
+}
+
+DetectorCore::DetectorCore(const Params& params, const NodeConfig& config, int device)
+    : width_(config.camera.width), height_(config.camera.height), params_(params) {
+  std::copy(config.R, config.R + 9, R_);
+  std::copy(config.t, config.t + 3, t_);
+  init(config.cam, device);
+}
+
+void DetectorCore::init(const at_camera& cam, int device) {
   at_config cfg;
-  at_config_default(&cfg, width, height);  // the node's detector settings (:139-147), TAGSIZE
+  at_config_default(&cfg, width_, height_);  // the node's detector settings (:139-147), TAGSIZE
   cfg.device = device;
   const int rc = at_create(&cfg, &cam, &det_);
   if (rc != AT_OK) throw std::runtime_error(std::string("at_create: ") + at_strerror(rc));
-  dets_.resize(1024);
-  poses_.resize(1024);
+  dets_.resize(at_max_detections());  // every detection of a frame (no truncation)
+  poses_.resize(at_max_detections());
   if (params_.measurement_mode) {
     csv_path_ = params_.timing_csv_path;
     if (csv_path_.empty()) {  // apriltags_timing_YYYYMMDD_hhmmss.csv (:565-574)
@@ -339,6 +486,7 @@ DetectorCore::DetectorCore(int width, int height, const Params& params, const at
 }
 
 DetectorCore::~DetectorCore() {
+  image_queue_.reset();  // stops the publisher thread (the reference stops its queue, :80-82)
   if (csv_) std::fclose(csv_);
   at_destroy(det_);
 }
@@ -372,8 +520,11 @@ int DetectorCore::process(const uint8_t* frame, at_pixfmt fmt, double stamp_s, d
   }
   out->proto = encode_apriltag_list(out->tags.data(), (int)out->tags.size(), stamp_s);
   if (annotate && fmt == AT_FMT_BGR8) {
-    annotate->assign(frame, frame + (size_t)width_ * height_ * 3);
-    draw_detection_outlines(annotate->data(), width_, height_, out->detections.data(), n);
+    // draw_detection_outlines (:411) on the GPU, on the copy of the frame at_detect
+    // staged in HBM: no host copy of the frame, no host drawing
+    annotate->resize((size_t)width_ * height_ * 3);
+    const int arc = at_annotate_staged(det_, 0, out->detections.data(), n, annotate->data());
+    if (arc != AT_OK) return arc;
   }
   const auto nt0 = clk::now();
   if (send_networktables) send_networktables(ctx, out->networktables_pose_data, out->proto);
@@ -382,7 +533,15 @@ int DetectorCore::process(const uint8_t* frame, at_pixfmt fmt, double stamp_s, d
   const auto pp1 = clk::now();
   if (publish_camera) publish_camera(ctx, out->camera);
   const auto pc1 = clk::now();
-  if (publish_image && annotate && !annotate->empty()) publish_image(ctx, *annotate);
+  if (publish_image && annotate && !annotate->empty()) {
+    if (!image_queue_) {
+      auto pub = publish_image;
+      void* c = ctx;
+      image_queue_.reset(new PublisherQueue<StampedImage>(
+          [pub, c](const StampedImage& img) { pub(c, img.bgr, img.stamp_s); }, 2));
+    }
+    image_queue_->enqueue(StampedImage{*annotate, stamp_s});  // image_pub_queue_->enqueue (:514-518)
+  }
   const auto pi1 = clk::now();
   if (csv_) {  // latency,det,publish_pose,publish_camera_pose,publish_image,networktables,processing (:526-552)
     std::fprintf(csv_, "%lld,%lld,%lld,%lld,%lld,%lld,%lld\n", (long long)std::llround((receive_s - stamp_s) * 1e6),
@@ -423,6 +582,58 @@ int at_node_load_extrinsics(const char* path, const char* serial, double* R, dou
 
 void at_node_draw_detection_outlines(uint8_t* bgr, int width, int height, const at_detection* dets, int n) {
   at_node::draw_detection_outlines(bgr, width, height, dets, n);
+}
+
+// ConfigLoader::getCameraConfig: width, height, frame_rate and the location string.
+int at_node_load_camera_config(const char* path, const char* serial, int* width, int* height, int* frame_rate,
+                               char* location, size_t cap) {
+  at_node::CameraConfig c;
+  if (!at_node::load_camera_config(path, serial, &c)) return -1;
+  if (width) *width = c.width;
+  if (height) *height = c.height;
+  if (frame_rate) *frame_rate = c.frame_rate;
+  if (location && cap) {
+    std::strncpy(location, c.location.c_str(), cap - 1);
+    location[cap - 1] = 0;
+  }
+  return 0;
+}
+
+// package_share_directory("vision_config_data") through $AMENT_PREFIX_PATH.
+long long at_node_package_share_directory(const char* package, char* out, size_t cap) {
+  const std::string s = at_node::package_share_directory(package);
+  if (out && cap) {
+    std::strncpy(out, s.c_str(), cap - 1);
+    out[cap - 1] = 0;
+  }
+  return (long long)s.size();
+}
+
+// resolve_node_config: W x H, intrinsics (fx fy cx cy k1 k2 p1 p2 k3), extrinsics.
+int at_node_resolve_config(const char* serial, const char* share_dir, int* wh, at_camera* cam, double* R, double* t,
+                           int* have_extrinsics) {
+  at_node::NodeConfig nc;
+  if (!at_node::resolve_node_config(serial, share_dir ? share_dir : "", &nc, nullptr)) return -1;
+  if (wh) {
+    wh[0] = nc.camera.width;
+    wh[1] = nc.camera.height;
+  }
+  if (cam) *cam = nc.cam;
+  if (R) std::copy(nc.R, nc.R + 9, R);
+  if (t) std::copy(nc.t, nc.t + 3, t);
+  if (have_extrinsics) *have_extrinsics = nc.have_extrinsics;
+  return 0;
+}
+
+// apply_cpu_pinning_and_scheduling on the calling thread; 1 = applied and verified.
+int at_node_apply_cpu_pinning(int pin_to_core, int priority, char* log, size_t cap) {
+  std::string msg;
+  const bool ok = at_node::apply_cpu_pinning_and_scheduling(pin_to_core, priority, &msg);
+  if (log && cap) {
+    std::strncpy(log, msg.c_str(), cap - 1);
+    log[cap - 1] = 0;
+  }
+  return ok ? 1 : 0;
 }
 
 }  // extern "C"

@@ -6,7 +6,11 @@
 // parameters (topic_name, camera_serial, publish_images_to_topic, publish_pose_to_topic,
 // pin_to_core, priority, measurement_mode, timing_csv_path), subscription QoS (depth 1,
 // best effort, volatile, 50 ms deadline), TagDetectionArray publishers on <pose> (robot
-// frame) and <pose>_camera, the outlined bgr8 image, calibration / system_config lookup.
+// frame) and <pose>_camera, the outlined bgr8 image through a drop-oldest publisher
+// queue.  Set-up as the reference's (apriltags_cuda_detector.cu:137-193, 601-605): frame
+// W x H, intrinsics and extrinsics from the camera serial's records in
+// vision_config_data's share directory (ament_index), then CPU pinning + SCHED_FIFO.
+// The launch file (launch_vision.py:283-305) passes nothing else.
 // The NetworkTables double array and ApriltagListProto are handed to the reference's
 // AprilTagDataSender (wpilib) when the workspace provides it (send_networktables hook).
 #include <cstring>
@@ -14,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "ament_index_cpp/get_package_share_directory.hpp"
 #include "apriltags_cuda/msg/tag_detection.hpp"
 #include "apriltags_cuda/msg/tag_detection_array.hpp"
 #include "at_node.h"
@@ -32,20 +37,27 @@ class ApriltagsAmdNode : public rclcpp::Node {
     p.priority = declare_parameter<int>("priority", p.priority);
     p.measurement_mode = declare_parameter<bool>("measurement_mode", p.measurement_mode);
     p.timing_csv_path = declare_parameter<std::string>("timing_csv_path", p.timing_csv_path);
-    const std::string calib_dir = declare_parameter<std::string>("calibration_dir", "calibration");
-    const std::string sys_cfg = declare_parameter<std::string>("system_config", "system_config.json");
-    const int width = declare_parameter<int>("frame_width", 1280);
-    const int height = declare_parameter<int>("frame_height", 720);
-
-    at_camera cam{};
+    // optional override of the share directory (not passed by the launch file)
+    std::string share_dir = declare_parameter<std::string>("vision_config_dir", "");
+    if (share_dir.empty()) {
+      try {
+        share_dir = ament_index_cpp::get_package_share_directory("vision_config_data");
+      } catch (const std::exception& e) {
+        RCLCPP_ERROR(get_logger(), "vision_config_data: %s", e.what());
+      }
+    }
+    at_node::NodeConfig config;
     std::string err;
-    if (!at_node::load_camera_calibration(calib_dir, p.camera_serial, &cam, &err))
-      throw std::runtime_error("calibration: " + err);
-    double R[9], t[3];
-    std::string location;
-    if (!at_node::load_extrinsics(sys_cfg, p.camera_serial, R, t, &location))
+    if (!at_node::resolve_node_config(p.camera_serial, share_dir, &config, &err)) {
+      RCLCPP_ERROR(get_logger(), "%s", err.c_str());
+      throw std::runtime_error(err);  // as setup_apriltags (:162-169)
+    }
+    if (!config.have_extrinsics)
       RCLCPP_ERROR(get_logger(), "no extrinsics for camera %s: identity / zero", p.camera_serial.c_str());
-    core_ = std::make_unique<at_node::DetectorCore>(width, height, p, cam, R, t);
+    RCLCPP_INFO(get_logger(), "Using camera config dimensions: %dx%d for serial %s", config.camera.width,
+                config.camera.height, p.camera_serial.c_str());
+    const int width = config.camera.width, height = config.camera.height;
+    core_ = std::make_unique<at_node::DetectorCore>(p, config);
     core_->ctx = this;
     core_->publish_robot = [](void* c, const std::vector<at_node::TagDetectionMsg>& v) {
       static_cast<ApriltagsAmdNode*>(c)->pose_pub_->publish(to_msg(v));
@@ -53,10 +65,10 @@ class ApriltagsAmdNode : public rclcpp::Node {
     core_->publish_camera = [](void* c, const std::vector<at_node::TagDetectionMsg>& v) {
       static_cast<ApriltagsAmdNode*>(c)->camera_pose_pub_->publish(to_msg(v));
     };
-    core_->publish_image = [](void* c, const std::vector<uint8_t>& bgr) {
-      auto* self = static_cast<ApriltagsAmdNode*>(c);
+    core_->publish_image = [](void* c, const std::vector<uint8_t>& bgr, double stamp_s) {
+      auto* self = static_cast<ApriltagsAmdNode*>(c);  // publisher-queue thread
       auto msg = std::make_unique<sensor_msgs::msg::Image>();
-      msg->header = self->last_header_;
+      msg->header.stamp = rclcpp::Time(static_cast<int64_t>(stamp_s * 1e9));  // image_capture_time (:516)
       msg->header.frame_id = "apriltag_detections";
       msg->width = self->width_;
       msg->height = self->height_;
@@ -73,6 +85,9 @@ class ApriltagsAmdNode : public rclcpp::Node {
     pose_pub_ = create_publisher<apriltags_cuda::msg::TagDetectionArray>(p.publish_pose_to_topic, 10);
     camera_pose_pub_ = create_publisher<apriltags_cuda::msg::TagDetectionArray>(core_->camera_pose_topic(), 10);
     image_pub_ = create_publisher<sensor_msgs::msg::Image>(p.publish_images_to_topic, 10);
+    std::string sched_log;  // applyCpuPinningAndScheduling (:601-605)
+    at_node::apply_cpu_pinning_and_scheduling(p.pin_to_core, p.priority, &sched_log);
+    RCLCPP_INFO(get_logger(), "%s", sched_log.c_str());
   }
 
  private:
@@ -109,7 +124,6 @@ class ApriltagsAmdNode : public rclcpp::Node {
       for (int y = 0; y < height_; ++y) std::memcpy(packed_.data() + row * y, m->data.data() + (size_t)m->step * y, row);
       frame = packed_.data();
     }
-    last_header_ = m->header;
     const double stamp = rclcpp::Time(m->header.stamp).seconds();
     at_node::FrameOutputs out;
     const int rc = core_->process(frame, fmt, stamp, now().seconds(), &out, fmt == AT_FMT_BGR8 ? &image_ : nullptr);
@@ -118,7 +132,6 @@ class ApriltagsAmdNode : public rclcpp::Node {
 
   std::unique_ptr<at_node::DetectorCore> core_;
   int width_ = 0, height_ = 0;
-  std_msgs::msg::Header last_header_;
   std::vector<uint8_t> packed_, image_;
   rclcpp::Subscription<sensor_msgs::msg::Image>::SharedPtr sub_;
   rclcpp::Publisher<apriltags_cuda::msg::TagDetectionArray>::SharedPtr pose_pub_, camera_pose_pub_;

@@ -113,7 +113,7 @@ using namespace at;
 // words, then scalars
 enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlPerFrame };
 enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
-       kCtlScalars = kCtlNcls + kNumCls };
+       kCtlDetHead = kCtlNcls + kNumCls, kCtlScalars = kCtlDetHead + 1 };
 
 static constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 
@@ -136,11 +136,14 @@ struct at_detector {
   uint32_t* d_ctrl;         // control block (zeroed each batch)
   size_t ctrl_words;
   uint32_t* h_ctrl;         // pinned copy of the control block
-  DevDetection* h_dets;     // pinned [B][kMaxDets]
-  std::vector<at_pose> poses;   // [B][kMaxDets] poses of the last collected batch (id order)
-  std::vector<int> nposes;      // [B]
+  DevDetection* h_dets;     // pinned [det_cap]: the batch-wide candidate pool (mapped)
+  // results of the last collected batch: frame f's detections are the pool records
+  // res_idx[res_off[f] .. res_off[f] + res_n[f]) in id order (after reconcile)
+  std::vector<int> res_idx, res_off, res_n;
   int last_nframes;
   int last_fmt;
+  int last_staged;          // the last batch's frames were host frames staged in d_in (at_detect*)
+  int last_gp;              // the last batch ran the game-piece preprocessing (k_gp_pre)
   int pending;
   hipEvent_t ev_done;
   hipEvent_t ev_ext;                      // at_stream_wait: recorded on the producer's stream
@@ -392,7 +395,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.wcap = (uint32_t)(B * kMaxPairs);
   b.work = (uint32_t*)dalloc((size_t)kNumCls * B * kMaxPairs * 4);
   b.probe = (uint64_t*)dalloc(kProbeWords * 8);
-  b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
+  b.det_cap = (uint32_t)std::max<size_t>(kMaxDets, (size_t)kDetPoolPerFrame * B);
+  b.dets = (DevDetection*)dalloc(b.det_cap * sizeof(DevDetection));
   b.quads = (QuadRecord*)dalloc(B * kMaxPairs * sizeof(QuadRecord));
   d->ctrl_words = kCtlPerFrame * B + kCtlScalars;
   d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
@@ -409,21 +413,25 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.workhead_small = sc + kCtlWorkheadSmall;
   b.blob_pts = sc + kCtlBlobPts;
   b.ncls = sc + kCtlNcls;
+  b.det_head = sc + kCtlDetHead;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)
   b.s_pk = (uint64_t*)dalloc((size_t)d->nblobwg * (kSortCap / 2) * 8);
-  b.rsamp = (double*)dalloc((size_t)d->nblobwg * kDecodeGridPerBlobWg * 2 * (kMaxRefineSamples - kLdsRefine) * 8);
+  // refine samples past LDS, one region per k_decode workgroup of the grid
+  // launch_pipeline uses for a full batch (decode_grid)
+  b.rsamp = (double*)dalloc((size_t)decode_grid(d->nblobwg, d->B) * 2 * (kMaxRefineSamples - kLdsRefine) * 8);
   if (oom) return fail(AT_E_NOMEM);
   // frame pointer table: fine-grained mapped host memory read by k_pre directly
   // (no host-to-device copy per batch; the GPU does not cache it)
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     return fail(AT_E_NOMEM);
   if (hipHostGetDevicePointer((void**)&b.frames, (void*)d->h_ftab, 0) != hipSuccess) return fail(AT_E_HIP);
-  d->poses.assign(B * kMaxDets, at_pose{});
-  d->nposes.assign(B, 0);
+  d->res_idx.assign(b.det_cap, 0);
+  d->res_off.assign(B, 0);
+  d->res_n.assign(B, 0);
   if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocMapped) != hipSuccess) return fail(AT_E_NOMEM);
-  if (hipHostMalloc((void**)&d->h_dets, B * kMaxDets * sizeof(DevDetection), hipHostMallocMapped) != hipSuccess)
+  if (hipHostMalloc((void**)&d->h_dets, b.det_cap * sizeof(DevDetection), hipHostMallocMapped) != hipSuccess)
     return fail(AT_E_NOMEM);
   // device views of the mapped host result buffers (k_decode / k_pose write them)
   if (hipHostGetDevicePointer((void**)&b.hdets, d->h_dets, 0) != hipSuccess ||
@@ -492,14 +500,22 @@ static int prefer_smaller(int pref, double q0, double q1) {
   return 0;
 }
 
-static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int cap, at_pose* poses) {
-  // the reference's zarray operations on an index array (the 272-byte records stay
+static void write_detection(const DevDetection& v, at_detection* o) {
+  o->id = v.id;
+  o->hamming = v.hamming;
+  o->decision_margin = v.decision_margin;
+  memcpy(o->H, v.H, sizeof(o->H));
+  memcpy(o->c, v.c, sizeof(o->c));
+  memcpy(o->p, v.p, sizeof(o->p));
+}
+
+// One frame's candidates: idx[0..ncand) are pool indices; on return idx[0..n) are
+// the detections in id order (n is returned).
+static int host_tail(const DevDetection* cand, int* idx, int ncand, at_detection* out, int cap) {
+  // the reference's zarray operations on an index array (the 280-byte records stay
   // where k_decode / k_pose wrote them): order by blob rank, reconcile with the
   // same swap-with-last removals, stable sort by id
-  thread_local std::vector<int> idx;
-  idx.resize((size_t)ncand);
-  for (int i = 0; i < ncand; i++) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cand[a].blob_rank < cand[b].blob_rank; });
+  std::stable_sort(idx, idx + ncand, [&](int a, int b) { return cand[a].blob_rank < cand[b].blob_rank; });
   int n = ncand;
   for (int i0 = 0; i0 < n; i0++) {
     for (int i1 = i0 + 1; i1 < n; i1++) {
@@ -523,25 +539,8 @@ static int host_tail(const DevDetection* cand, int ncand, at_detection* out, int
       }
     }
   }
-  idx.resize((size_t)n);
-  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cand[a].id < cand[b].id; });
-  for (int i = 0; i < n && i < kMaxDets; i++) {
-    const DevDetection& v = cand[idx[i]];
-    poses[i].id = v.id;
-    memcpy(poses[i].R, v.pose_R, sizeof(poses[i].R));
-    memcpy(poses[i].t, v.pose_t, sizeof(poses[i].t));
-    poses[i].err = v.pose_err[0] <= v.pose_err[1] ? v.pose_err[0] : v.pose_err[1];  // estimate_tag_pose
-  }
-  for (int i = 0; i < n && i < cap; i++) {
-    const DevDetection& v = cand[idx[i]];
-    at_detection& o = out[i];
-    o.id = v.id;
-    o.hamming = v.hamming;
-    o.decision_margin = v.decision_margin;
-    memcpy(o.H, v.H, sizeof(o.H));
-    memcpy(o.c, v.c, sizeof(o.c));
-    memcpy(o.p, v.p, sizeof(o.p));
-  }
+  std::stable_sort(idx, idx + n, [&](int a, int b) { return cand[a].id < cand[b].id; });
+  for (int i = 0; i < n && i < cap; i++) write_detection(cand[idx[i]], out + i);
   return n;
 }
 
@@ -652,6 +651,7 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   HIPCHK(hipEventRecord(d->ev_done, st));
   d->last_nframes = nframes;
   d->last_fmt = fmt;
+  d->last_gp = d->prm.gp_c && fmt == AT_FMT_BGR8;
   d->pending = 1;
   return AT_OK;
 }
@@ -683,17 +683,33 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   }
   const int B = d->B;
   int rc = AT_OK;
-  for (int f = 0; f < d->last_nframes; f++) {
+  // group the pool's candidates by frame (counting sort, pool order kept)
+  const int nf = d->last_nframes;
+  const int total = (int)std::min<uint32_t>(d->h_ctrl[kCtlPerFrame * B + kCtlDetHead], d->d.det_cap);
+  int* idx = d->res_idx.data();
+  int* off = d->res_off.data();
+  int* cnt = d->res_n.data();
+  for (int f = 0; f < nf; f++) cnt[f] = 0;
+  for (int i = 0; i < total; i++) cnt[d->h_dets[i].frame]++;
+  for (int f = 0, o = 0; f < nf; f++) {
+    off[f] = o;
+    o += cnt[f];
+    cnt[f] = 0;
+  }
+  for (int i = 0; i < total; i++) {
+    const int f = d->h_dets[i].frame;
+    idx[off[f] + cnt[f]++] = i;
+  }
+  for (int f = 0; f < nf; f++) {
     const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
-    const int ncand = (int)std::min<uint32_t>(d->h_ctrl[kCtlNdets * B + f], (uint32_t)kMaxDets);
     int n = 0;
     if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow)) {
       rc = AT_E_CAPACITY;
     } else {
-      n = host_tail(d->h_dets + (size_t)f * kMaxDets, ncand, out ? out + (size_t)f * cap_per_frame : nullptr,
-                    out ? cap_per_frame : 0, d->poses.data() + (size_t)f * kMaxDets);
+      n = host_tail(d->h_dets, idx + off[f], cnt[f], out ? out + (size_t)f * cap_per_frame : nullptr,
+                    out ? cap_per_frame : 0);
     }
-    d->nposes[f] = d->prm.tag_size > 0 ? std::min(n, kMaxDets) : 0;
+    cnt[f] = n;
     if (n_per_frame) n_per_frame[f] = n;
   }
   d->host_tail_us += now_us() - t1;
@@ -720,6 +736,7 @@ int at_detect_batch(at_detector* d, const uint8_t* const* frames, int nframes, a
   }
   int rc = enqueue(d, nframes, fmt);
   if (rc) return rc;
+  d->last_staged = 1;
   return collect(d, out, cap_per_frame, n_per_frame);
 }
 
@@ -738,7 +755,9 @@ int at_enqueue_device(at_detector* d, const void* d_frames, size_t frame_stride,
   HIPCHK(hipSetDevice(d->device));
   if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));  // pinned buffers are reused
   for (int f = 0; f < nframes; f++) d->h_ftab[f] = (const uint8_t*)d_frames + (size_t)f * frame_stride;
-  return enqueue(d, nframes, fmt);
+  const int rc = enqueue(d, nframes, fmt);
+  d->last_staged = 0;
+  return rc;
 }
 
 int at_stream_wait(at_detector* d, void* stream) {
@@ -826,10 +845,28 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
 int at_poses(at_detector* d, int frame, at_pose* out, int cap) {
   if (!d || frame < 0 || frame >= d->last_nframes || (cap > 0 && !out)) return AT_E_INVALID;
   if (d->pending) return AT_E_INVALID;  // collect first
-  const int n = d->nposes[frame];
-  for (int i = 0; i < n && i < cap; i++) out[i] = d->poses[(size_t)frame * kMaxDets + i];
+  if (!(d->prm.tag_size > 0)) return 0;
+  const int n = d->res_n[frame];
+  for (int i = 0; i < n && i < cap; i++) {
+    const DevDetection& v = d->h_dets[d->res_idx[d->res_off[frame] + i]];
+    at_pose& p = out[i];
+    p.id = v.id;
+    memcpy(p.R, v.pose_R, sizeof(p.R));
+    memcpy(p.t, v.pose_t, sizeof(p.t));
+    p.err = v.pose_err[0] <= v.pose_err[1] ? v.pose_err[0] : v.pose_err[1];  // estimate_tag_pose
+  }
   return n;
 }
+
+int at_detections(at_detector* d, int frame, at_detection* out, int cap) {
+  if (!d || frame < 0 || frame >= d->last_nframes || (cap > 0 && !out)) return AT_E_INVALID;
+  if (d->pending) return AT_E_INVALID;
+  const int n = d->res_n[frame];
+  for (int i = 0; i < n && i < cap; i++) write_detection(d->h_dets[d->res_idx[d->res_off[frame] + i]], out + i);
+  return n;
+}
+
+int at_max_detections(void) { return kMaxDets; }
 
 int at_tag_detections(const at_pose* poses, int n, const double* extr_R, const double* extr_t,
                       at_tag_detection* out) {
@@ -926,6 +963,18 @@ int at_draw_outlines_device(at_detector* d, const at_detection* dets, int n, uin
   return AT_OK;
 }
 
+int at_annotate_staged(at_detector* d, int frame, const at_detection* dets, int n, uint8_t* bgr_out) {
+  if (!d || !bgr_out || n < 0 || (n > 0 && !dets)) return AT_E_INVALID;
+  if (!d->last_staged || d->last_fmt != AT_FMT_BGR8 || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
+  HIPCHK(hipSetDevice(d->device));
+  if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));
+  uint8_t* img = d->d_in + (size_t)frame * d->in_stride;
+  const int rc = at_draw_outlines_device(d, dets, n, img);
+  if (rc != AT_OK) return rc;
+  HIPCHK(hipMemcpy(bgr_out, img, (size_t)d->g.W * d->g.H * 3, hipMemcpyDeviceToHost));
+  return AT_OK;
+}
+
 // ---- shared game-piece preprocessing ---------------------
 static void drop_graphs(at_detector* d) {
   for (auto& kv : d->graphs) (void)hipGraphExecDestroy(kv.second);
@@ -954,13 +1003,13 @@ int at_gp_enable(at_detector* d, int out_width, int out_height, int channels) {
   d->prm.gp_w = out_width;
   d->prm.gp_h = out_height;
   d->prm.gp_c = channels;
+  d->last_gp = 0;  // no tensor until a BGR8 batch has produced one
   drop_graphs(d);  // the captured sequences carry the old parameters
   return AT_OK;
 }
 
 int at_gp_tensor(at_detector* d, int frame, const float** dev_ptr) {
-  if (!d || !dev_ptr || !d->prm.gp_c || frame < 0 || frame >= d->last_nframes || d->last_fmt != AT_FMT_BGR8)
-    return AT_E_INVALID;
+  if (!d || !dev_ptr || !d->prm.gp_c || !d->last_gp || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
   *dev_ptr = d->d.gp_out + (size_t)frame * d->prm.gp_c * d->prm.gp_w * d->prm.gp_h;
   return AT_OK;
 }

@@ -52,6 +52,12 @@ constexpr int kNMaxima = 10;
 constexpr int kMaxRefineSamples = 1536;
 constexpr int kLdsRefine = 256;
 constexpr int kDecodeGridPerBlobWg = 8;  // k_decode workgroups <= nblobwg * this
+// k_decode's persistent grid for a batch of B frames: enough one-wave groups for
+// every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
+inline int decode_grid(int nblobwg, int B) {
+  const int hi = nblobwg * kDecodeGridPerBlobWg, want = 64 * B;
+  return nblobwg * 2 > (want < hi ? want : hi) ? nblobwg * 2 : (want < hi ? want : hi);
+}
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
 constexpr int kNumStages = 12;
@@ -76,7 +82,13 @@ constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config
 // one detection, so sizing both queues by kMaxPairs makes neither of them a cap:
 // the reference decodes every quad (apriltag_detect.cu:618-663).
 constexpr int kQuadCandPerFrame = kMaxPairs;  // accepted quads queued for decode, per frame
-constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections per frame (before reconcile)
+constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections one frame can have (before reconcile)
+// Candidate detections live in one batch-wide pool filled through an atomic cursor
+// (DevBufs::det_head): max(kMaxDets, kDetPoolPerFrame * B) records, so one frame can
+// still reach kMaxDets while the pinned result buffer follows the batch's typical
+// count instead of B * kMaxDets (a pool that fills flags kStatusDetsOverflow on the
+// frames whose candidates did not fit).
+constexpr int kDetPoolPerFrame = 128;
 constexpr int kMaxCodes = 1024;               // codebook entries (tag36h11: 587)
 constexpr int kMaxFamilyBits = 64;
 
@@ -139,7 +151,9 @@ struct KernelTimer {
 
 // One detection candidate as produced on the device (before reconcile).
 struct DevDetection {
-  int32_t id, hamming;
+  int32_t id;
+  int16_t hamming;
+  uint16_t frame;  // frame of the batch (the pool is batch-wide)
   float decision_margin;
   int32_t blob_rank;
   double H[9];
@@ -201,12 +215,14 @@ struct DevBufs {
   uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair
   uint32_t* work;     // [kNumCls][wcap] (frame << 16) | rank of candidate pairs, by size class
   uint32_t wcap;      // B * kMaxPairs
-  DevDetection* dets; // [B][kMaxDets]
+  DevDetection* dets; // [det_cap] batch-wide pool of candidates (DevDetection::frame)
+  uint32_t det_cap;
+  uint32_t* det_head; // [1] pool cursor (control block)
   // zero-copy results: the detections (k_decode, poses added by k_pose) and the
   // control block (copied by k_pose) are also written straight into the
   // caller-visible pinned host buffers (device pointers of mapped host memory),
   // which replaces two device-to-host copies per batch
-  DevDetection* hdets;  // [B][kMaxDets] host
+  DevDetection* hdets;  // [det_cap] host
   uint32_t* hctrl;      // [ctrl_words] host
   uint32_t* ctrl;       // device control block base
   uint32_t ctrl_words;
@@ -214,7 +230,7 @@ struct DevBufs {
   // control block (zeroed every batch)
   uint32_t* npts;     // [B]
   uint32_t* npairs;   // [B]
-  uint32_t* ndets;    // [B]
+  uint32_t* ndets;    // [B] candidates per frame (pool entries + overflowed ones)
   uint32_t* nquads;   // [B]
   uint32_t* status;   // [B]
   uint32_t* ncls;     // [kNumCls] candidate pairs per size class

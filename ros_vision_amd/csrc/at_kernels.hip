@@ -3362,10 +3362,12 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
           const int tcy = (i < 2) ? 1 : -1;
           hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
         }
-        const uint32_t di = atomicAdd(b.ndets + f, 1u);
-        if (di < (uint32_t)kMaxDets) {
-          b.dets[(size_t)f * kMaxDets + di] = d;
-          b.hdets[(size_t)f * kMaxDets + di] = d;  // pose fields follow from k_pose
+        d.frame = (uint16_t)f;
+        atomicAdd(b.ndets + f, 1u);
+        const uint32_t di = atomicAdd(b.det_head, 1u);
+        if (di < b.det_cap) {
+          b.dets[di] = d;
+          b.hdets[di] = d;  // pose fields follow from k_pose
         }
         else atomicOr(b.status + f, kStatusDetsOverflow);
       }
@@ -3454,22 +3456,22 @@ constexpr int kPoseGroupsPerFrame = 8;  // 128 detections per pass, looped beyon
 // per detection, one bracket each.
 template <bool WAVE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AT_POSE_WAVES))) void k_pose(DevBufs b, Params prm) {
-  const int f = blockIdx.y;
   const int sub = (int)(threadIdx.x % kPoseLanes);
-  // the control block is final once k_decode has finished: block (0, 0) hands it
-  // to the host (replaces a device-to-host copy)
-  if (blockIdx.x == 0 && blockIdx.y == 0)
+  // the control block is final once k_decode has finished: block 0 hands it to
+  // the host (replaces a device-to-host copy)
+  if (blockIdx.x == 0)
     for (uint32_t w = threadIdx.x; w < b.ctrl_words; w += 64) b.hctrl[w] = b.ctrl[w];
-  const uint32_t n = min(b.ndets[f], (uint32_t)kMaxDets);
+  // the batch's candidates, whatever their frame (the pool is batch-wide)
+  const uint32_t n = min(*b.det_head, b.det_cap);
   constexpr uint32_t kPer = WAVE ? 1 : 64 / kPoseLanes;  // detections per wave
   for (uint32_t i = blockIdx.x * kPer + (WAVE ? 0 : threadIdx.x / kPoseLanes); i < n;  // uniform across the quad
        i += gridDim.x * kPer) {
-    DevDetection& d = b.dets[(size_t)f * kMaxDets + i];
+    DevDetection& d = b.dets[i];
     double R[9], t[3], err[2];
     pose::estimate_tag_pose<WAVE>(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
-                                  (prm.probe && f == 0 && i == 0 && threadIdx.x == 0) ? b.probe + 16 : nullptr);
+                                  (prm.probe && i == 0 && threadIdx.x == 0) ? b.probe + 16 : nullptr);
     if (WAVE ? threadIdx.x == 0 : sub == 0) {
-      DevDetection& h = b.hdets[(size_t)f * kMaxDets + i];
+      DevDetection& h = b.hdets[i];
 #pragma unroll
       for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
 #pragma unroll
@@ -3753,7 +3755,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups
     // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
-    const dim3 grd(std::max(nblobwg * 2, std::min(nblobwg * kDecodeGridPerBlobWg, 64 * B)));
+    const dim3 grd(decode_grid(nblobwg, B));
     if (on(10)) hipLaunchKernelGGL(k_decode, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
   }
   tk(10, st, 1);
@@ -3761,8 +3763,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(11, st, 0);
   // latency mode: a wave per detection; throughput mode: four lanes per detection
   if (prm.tag_size > 0 && on(11)) {
-    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_pose<true>, dim3(32, B), dim3(64), 0, st, b, prm);
-    else hipLaunchKernelGGL(k_pose<false>, dim3(kPoseGroupsPerFrame, B), dim3(64), 0, st, b, prm);
+    if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_pose<true>, dim3(32 * B), dim3(64), 0, st, b, prm);
+    else hipLaunchKernelGGL(k_pose<false>, dim3(kPoseGroupsPerFrame * B), dim3(64), 0, st, b, prm);
   }
   tk(11, st, 1);
   mark();

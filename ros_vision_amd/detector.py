@@ -33,7 +33,7 @@ EXPORTS = [
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
     "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
-    "at_draw_outlines_device",
+    "at_draw_outlines_device", "at_detections", "at_max_detections", "at_annotate_staged",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -188,6 +188,9 @@ def load_library(path: str = LIB_PATH):
                                               C.c_void_p]
     if hasattr(L, "at_draw_outlines_device"):
         L.at_draw_outlines_device.argtypes = [C.c_void_p, C.POINTER(AtDetection), C.c_int, C.c_void_p]
+    if hasattr(L, "at_detections"):  # (A/B builds of older sources lack them)
+        L.at_detections.argtypes = [C.c_void_p, C.c_int, C.POINTER(AtDetection), C.c_int]
+        L.at_annotate_staged.argtypes = [C.c_void_p, C.c_int, C.POINTER(AtDetection), C.c_int, C.c_void_p]
     _LIB = L
     return L
 
@@ -246,7 +249,7 @@ def _check(rc, what):
 class GpuDetector:
     """Drop-in for frc971::apriltag::GpuDetector on MI355X (one instance per camera)."""
 
-    MAX_DETECTIONS = 1024  # per frame returned to Python (the library keeps up to 4096 per frame)
+    MAX_DETECTIONS = 64  # per frame in the collect buffer; frames with more are fetched whole (at_detections)
     DEBUG_TAPS = False     # default of debug_taps (the parity tests turn it on for their module)
 
     def __init__(self, width, height, camera_matrix: CameraMatrix = TEST_CAMERA,
@@ -295,12 +298,21 @@ class GpuDetector:
         self.close()
 
     # ---- detection ---------------------------------------------------------
+    def _frame_records(self, f):
+        """at_detection records of frame f of the last batch (all of them: a frame with
+        more than the collect buffer holds is fetched again with at_detections)."""
+        n = self._n[f]
+        if n <= self._cap:
+            return [self._out[f * self._cap + i] for i in range(n)]
+        buf = (AtDetection * n)()
+        got = _check(load_library().at_detections(self._h, f, buf, n), "at_detections")
+        return list(buf[:got])
+
     def _unpack(self, nframes):
         res = []
         for f in range(nframes):
             dets = []
-            for i in range(min(self._n[f], self._cap)):
-                d = self._out[f * self._cap + i]
+            for d in self._frame_records(f):
                 dets.append(Detection(id=d.id, hamming=d.hamming, decision_margin=d.decision_margin,
                                       H=np.array(list(d.H)).reshape(3, 3), c=np.array(list(d.c)),
                                       p=np.array([[d.p[k][0], d.p[k][1]] for k in range(4)])))
@@ -359,10 +371,11 @@ class GpuDetector:
     def poses(self, frame=0):
         """Pose of each detection of `frame` of the last batch (same order as its
         detections), computed on the GPU (k_pose) when tag_size > 0."""
-        buf = (AtPose * self._cap)()
-        n = _check(load_library().at_poses(self._h, frame, buf, self._cap), "at_poses")
+        cap = max(self._n[frame], 1)
+        buf = (AtPose * cap)()
+        n = _check(load_library().at_poses(self._h, frame, buf, cap), "at_poses")
         return [Pose(id=b.id, R=np.array(list(b.R)).reshape(3, 3), t=np.array(list(b.t)), err=b.err)
-                for b in buf[:min(n, self._cap)]]
+                for b in buf[:min(n, cap)]]
 
     def collect(self, counts_only=False):
         """at_collect: wait for the batch, run the host tail.  The detections land in
@@ -421,14 +434,25 @@ class GpuDetector:
         """GpuDetector::Detections (apriltag_gpu.h:93), sorted by id."""
         return self._last[frame]
 
+    def _records_array(self, frame):
+        recs = self._frame_records(frame)
+        arr = (AtDetection * max(1, len(recs)))(*recs)
+        return arr, len(recs)
+
     def draw_outlines_device(self, bgr_ptr: int, frame=0):
         """at_draw_outlines_device: the annotated image of `frame` of the last batch
         (outlines and ids, apriltag_utils.cu:54-79) drawn onto the device-resident
         BGR8 image at `bgr_ptr` (width x height x 3)."""
-        n = min(self._n[frame], self._cap)
-        addr = C.addressof(self._out) + frame * self._cap * C.sizeof(AtDetection)
-        first = C.cast(C.c_void_p(addr), C.POINTER(AtDetection))
-        _check(load_library().at_draw_outlines_device(self._h, first, n, bgr_ptr), "at_draw_outlines_device")
+        arr, n = self._records_array(frame)
+        _check(load_library().at_draw_outlines_device(self._h, arr, n, bgr_ptr), "at_draw_outlines_device")
+
+    def annotate_staged(self, frame=0):
+        """at_annotate_staged: the annotated image of host BGR8 frame `frame` of the last
+        batch, drawn on its staged copy in HBM; returns it (H, W, 3) uint8."""
+        arr, n = self._records_array(frame)
+        out = np.empty((self.height, self.width, 3), np.uint8)
+        _check(load_library().at_annotate_staged(self._h, frame, arr, n, out.ctypes.data), "at_annotate_staged")
+        return out
 
     def frame_status(self, frame=0):
         return load_library().at_frame_status(self._h, frame)

@@ -37,7 +37,36 @@ def nodelib(built):
     L.at_node_load_extrinsics.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.c_char_p, C.c_size_t]
     L.at_node_draw_detection_outlines.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    L.at_node_load_camera_config.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                             C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
+    L.at_node_package_share_directory.restype = C.c_longlong
+    L.at_node_package_share_directory.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+    L.at_node_resolve_config.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(detector.AtCamera),
+                                         C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
     return L
+
+
+def make_share_tree(root, serial, width, height, location="center_front", extra_cameras=None):
+    """An install prefix holding vision_config_data the way ament_index finds it:
+    <prefix>/share/ament_index/resource_index/packages/vision_config_data (marker) and
+    <prefix>/share/vision_config_data/data/{system_config.json, calibration/...}
+    (the layout of src/vision_config_data, CMakeLists.txt installs data/)."""
+    prefix = root / "install"
+    (prefix / "share/ament_index/resource_index/packages").mkdir(parents=True)
+    (prefix / "share/ament_index/resource_index/packages/vision_config_data").write_text("")
+    data = prefix / "share/vision_config_data/data"
+    (data / "calibration").mkdir(parents=True)
+    cams = {serial: {"location": location, "format": "MJPG", "height": height, "width": width,
+                     "frame_rate": 30, "api_preference": "V4L2"}}
+    cams.update(extra_cameras or {})
+    (data / "system_config.json").write_text(json.dumps({
+        "camera_mounted_positions": cams,
+        "extrinsics": {location: {"rotation": [[0, 0, 1], [-1, 0, 0], [0, -1, 0]], "offset": [0.25, -0.1, 0.4]}},
+        "network_tables_config": {"table_address": "10.7.66.2", "table_name": "/SmartDashboard"}}))
+    (data / "calibration" / ("calibrationmatrix_%s.json" % serial)).write_text(json.dumps(
+        {"matrix": [[905.495617, 0, 609.916016], [0, 907.909470, 352.682645], [0, 0, 1]],
+         "disto": [[0.059238, -0.075154, -0.003801, 0.001113, 0.0]]}))
+    return prefix
 
 
 def proto_classes():
@@ -172,7 +201,7 @@ def test_mock_node_matches_python_node_and_oracle(built, oracle_mod, tmp_path):
                           "bgr8", "--frames", str(path), "--camera-serial", "S1", "--system-config", str(cfg),
                           "--measurement-csv", str(csv), "--proto-out", str(proto)],
                          check=True, capture_output=True, text=True, timeout=180).stdout
-    lines = [json.loads(l) for l in out.splitlines()]
+    lines = [json.loads(l) for l in out.splitlines()][1:]  # after the set-up line
     assert len(lines) == 2
     node = N.ApriltagsDetectorNode(W, H, parameters={"camera_serial": "S1"}, system_config_path=str(cfg))
     Msg = proto_classes()
@@ -245,3 +274,130 @@ def test_gpu_outlines_match_cpu_drawing(nodelib):
     dev2 = torch.from_numpy(base).cuda()
     assert L.at_draw_outlines_device(small._h, raw, 4, dev2.data_ptr()) == 0
     assert np.array_equal(dev2.cpu().numpy(), cpu)
+
+
+def test_camera_config_records(nodelib, tmp_path):
+    """ConfigLoader::getCameraConfig (vision_utils/config_loader.cpp:77-105, 158-170):
+    complete records only, integer width / height / frame_rate."""
+    cfg = tmp_path / "system_config.json"
+    full = {"location": "left_front", "format": "MJPG", "height": 1080, "width": 1920, "frame_rate": 30,
+            "api_preference": "V4L2"}
+    cfg.write_text(json.dumps({"camera_mounted_positions": {
+        "A": full, "B": dict(full, width=1280.0), "C": {k: v for k, v in full.items() if k != "format"},
+        "D": "legacy_location"}}))
+    w, h, fr = C.c_int(), C.c_int(), C.c_int()
+    loc = C.create_string_buffer(64)
+    assert nodelib.at_node_load_camera_config(str(cfg).encode(), b"A", w, h, fr, loc, 64) == 0
+    assert (w.value, h.value, fr.value, loc.value) == (1920, 1080, 30, b"left_front")
+    for serial in (b"B", b"C", b"D", b"missing"):  # skipped as the reference skips them
+        assert nodelib.at_node_load_camera_config(str(cfg).encode(), serial, w, h, fr, loc, 64) == -1
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src/vision_config_data/data"), reason="reference absent")
+def test_camera_config_of_the_reference_system_config(nodelib):
+    """The deployed records (src/vision_config_data/data/system_config.json:2-50):
+    1920x1080, 800x600 and 1280x800 cameras."""
+    path = b"/root/reference/src/vision_config_data/data/system_config.json"
+    w, h, fr = C.c_int(), C.c_int(), C.c_int()
+    loc = C.create_string_buffer(64)
+    want = {b"HBVCAM": (1920, 1080, b"center_front"), b"12": (800, 600, b"left_front"),
+            b"199": (1280, 800, b"left_back"), b"test_camera": (640, 480, b"center_front")}
+    for serial, (ww, hh, ll) in want.items():
+        assert nodelib.at_node_load_camera_config(path, serial, w, h, fr, loc, 64) == 0
+        assert (w.value, h.value, loc.value) == (ww, hh, ll)
+
+
+def test_resolve_node_config_through_ament_prefix(nodelib, tmp_path, monkeypatch):
+    """setup_apriltags (apriltags_cuda_detector.cu:137-193): vision_config_data found
+    through AMENT_PREFIX_PATH as ament_index_cpp does; W x H from the camera record,
+    intrinsics from data/calibration, extrinsics from data/system_config.json."""
+    from ros_vision_amd import detector as D
+    prefix = make_share_tree(tmp_path, "CAMX", 1920, 1080)
+    monkeypatch.setenv("AMENT_PREFIX_PATH", "/nonexistent:" + str(prefix))
+    buf = C.create_string_buffer(512)
+    assert nodelib.at_node_package_share_directory(b"vision_config_data", buf, 512) > 0
+    assert buf.value.decode() == str(prefix / "share/vision_config_data")
+    wh, cam, R, t, have = (C.c_int * 2)(), D.AtCamera(), (C.c_double * 9)(), (C.c_double * 3)(), C.c_int()
+    assert nodelib.at_node_resolve_config(b"CAMX", None, wh, C.byref(cam), R, t, C.byref(have)) == 0
+    assert list(wh) == [1920, 1080] and cam.fx == 905.495617 and cam.k2 == -0.075154 and have.value == 1
+    assert list(R) == [0, 0, 1, -1, 0, 0, 0, -1, 0] and list(t) == [0.25, -0.1, 0.4]
+    # the reference throws without the camera record or the calibration file
+    assert nodelib.at_node_resolve_config(b"UNKNOWN", None, wh, C.byref(cam), R, t, C.byref(have)) == -1
+    monkeypatch.setenv("AMENT_PREFIX_PATH", "/nonexistent")
+    assert nodelib.at_node_resolve_config(b"CAMX", None, wh, C.byref(cam), R, t, C.byref(have)) == -1
+    share = str(prefix / "share/vision_config_data").encode()  # explicit directory (fallback parameter)
+    assert nodelib.at_node_resolve_config(b"CAMX", share, wh, C.byref(cam), R, t, C.byref(have)) == 0
+
+
+def test_cpu_pinning_and_scheduling(built):
+    """ProcessScheduler::applyCpuPinningAndScheduling (process_scheduler.cpp:23-121) in a
+    child process: -1 disables; an out-of-range core fails; a valid core pins the
+    thread (SCHED_FIFO succeeds only with CAP_SYS_NICE, reported either way)."""
+    code = r"""
+import ctypes as C, os, sys, json
+sys.path.insert(0, %r)
+from ros_vision_amd import detector
+detector.load_library()
+L = C.CDLL(%r)
+L.at_node_apply_cpu_pinning.argtypes = [C.c_int, C.c_int, C.c_char_p, C.c_size_t]
+log = C.create_string_buffer(4096)
+out = {"off": L.at_node_apply_cpu_pinning(-1, 80, log, 4096)}
+out["bad_core"] = L.at_node_apply_cpu_pinning(10 ** 6, 80, log, 4096)
+core = sorted(os.sched_getaffinity(0))[0]
+out["pin"] = L.at_node_apply_cpu_pinning(core, 10, log, 4096)
+out["affinity"] = sorted(os.sched_getaffinity(0))
+out["core"] = core
+out["log"] = log.value.decode()
+print(json.dumps(out))
+""" % (ROOT, os.path.join(built, "libat_node.so"))
+    r = json.loads(subprocess.run([sys.executable, "-c", code], check=True, capture_output=True, text=True,
+                                  timeout=120).stdout.strip().splitlines()[-1])
+    assert r["off"] == 1 and r["bad_core"] == 0
+    assert r["affinity"] == [r["core"]]  # the calling thread is pinned whatever SCHED_FIFO did
+    assert ("SCHED_FIFO priority 10" in r["log"]) == (r["pin"] == 1)
+
+
+@pytest.mark.gpu
+def test_mock_node_from_camera_serial_1080p(built, oracle_mod, tmp_path, nodelib):
+    """given only --camera-serial (the launch file's parameters,
+    launch_vision.py:283-305) the node takes 1920x1080, the intrinsics and the extrinsics
+    from vision_config_data, detects like the oracle, and publishes the outlined image
+    drawn on the GPU on the staged frame -- pixel-identical to the CPU drawing."""
+    import ros_vision_amd as rva
+    from ros_vision_amd import synth
+    W, H = 1920, 1080
+    prefix = make_share_tree(tmp_path, "HBVCAM", W, H)
+    gray, _ = synth.render_board(W, H, seed=4300, ntags=24)
+    bgr = np.ascontiguousarray(np.repeat(gray[:, :, None], 3, axis=2))
+    path = tmp_path / "frames.raw"
+    bgr.tofile(path)
+    img_out = tmp_path / "annotated.raw"
+    env = dict(os.environ, AMENT_PREFIX_PATH=str(prefix))
+    out = subprocess.run([os.path.join(built, "at_mock_node"), "--camera-serial", "HBVCAM", "--format", "bgr8",
+                          "--frames", str(path), "--image-out", str(img_out), "--pin-to-core", "-1"],
+                         check=True, capture_output=True, text=True, timeout=180, env=env).stdout
+    lines = [json.loads(l) for l in out.splitlines()]
+    assert lines[0]["width"] == W and lines[0]["height"] == H and lines[0]["location"] == "center_front"
+    rec = lines[1]
+    orc = oracle_mod.Oracle(W, H)
+    orc.detect(bgr, rva.AT_FMT_BGR8)
+    want = orc.detections()
+    assert rec["status"] == 0 and len(want) >= 15
+    assert [d["id"] for d in rec["detections"]] == [d["id"] for d in want]
+    for a, b in zip(rec["detections"], want):
+        assert np.allclose(a["p"], b["p"], atol=1e-4) and np.array_equal(np.floor(a["p"]), np.floor(b["p"]))
+    # robot frame = R_ext t + t_ext of the camera-frame position
+    R = np.array([[0, 0, 1], [-1, 0, 0], [0, -1, 0]], float)
+    for r, c in zip(rec["robot"], rec["camera"]):
+        assert r[0] == c[0] and np.allclose(R @ np.array(c[1:]) + [0.25, -0.1, 0.4], r[1:], atol=1e-12)
+    # the GPU-annotated image == the node's CPU drawing of the same detections
+    dets = (rva.detector.AtDetection * len(want))()
+    for i, d in enumerate(rec["detections"]):
+        dets[i].id = d["id"]
+        for k in range(4):
+            dets[i].p[k][0], dets[i].p[k][1] = d["p"][k]
+        dets[i].c[0], dets[i].c[1] = d["c"]
+    cpu = bgr.copy()
+    nodelib.at_node_draw_detection_outlines(cpu.ctypes.data, W, H, dets, len(want))
+    gpu_img = np.fromfile(img_out, np.uint8).reshape(H, W, 3)
+    assert not np.array_equal(cpu, bgr) and np.array_equal(gpu_img, cpu)
