@@ -248,6 +248,7 @@ struct ao_state {
   int W, H, Wd, Hd;
   int min_tag_width;
   int status;
+  int n_pts_pairs; /* >= 0: points of the first 4096 pairs (capacity-capped frame) */
   uint8_t *gray, *dec, *thr;
   uint8_t *mm_unf, *mm; /* uchar2 tiles */
   uint32_t *parent, *labels, *sizes;
@@ -617,7 +618,8 @@ static void stage_select(ao_state *s) {
    * theta = llrintf((atan2f(y - cy, x - cx) + pi) * 8e6) */
   int n = 0, q = -1;
   uint64_t prev = ~0ULL;
-  for (int i = 0; i < s->n_pts; i++) {
+  const int npts = s->n_pts_pairs >= 0 ? s->n_pts_pairs : s->n_pts;  /* points of the kept pairs */
+  for (int i = 0; i < npts; i++) {
     const uint64_t k = s->pts[i], r01 = (k >> 24) & 0xffffffffffULL;
     if (r01 != prev) { q++; prev = r01; }
     const uint32_t bi = (uint32_t)q & 0xfff;
@@ -1351,10 +1353,20 @@ static void reconcile(ao_state *s) {
 int ao_detect(ao_state *s, const uint8_t *frame, int pixfmt) {
   s->status = 0;
   s->n_pts = s->n_pairs = s->n_sel = s->n_peaks = s->n_fq = s->n_quads = s->n_dets = 0;
+  s->n_pts_pairs = -1;
   stage_threshold(s, frame, pixfmt);
   stage_ccl(s);
   stage_boundary(s);
-  if (s->n_pairs > 4096) { s->status = -3; return -3; } /* 12-bit blob index (points.h:183-193) */
+  if (s->n_pairs > 4096) {
+    /* More pairs than the 12-bit blob index holds (points.h:183-193; the reference
+     * overflows its 2048-entry extents buffer here, apriltag_gpu.cu:129,899-902:
+     * undefined).  This build keeps the first 4096 pairs in rank order (rep01
+     * ascending, P2's order), drops the points of the others and reports the
+     * capacity status with the kept pairs' detections. */
+    s->status = -3;
+    s->n_pairs = 4096;
+    s->n_pts_pairs = (int)(s->ext[4095].starting_offset + s->ext[4095].count);
+  }
   stage_select(s);
   stage_linefit(s);
   stage_fitquads(s);

@@ -703,6 +703,7 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   for (int f = 0; f < nf; f++) {
     const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
     int n = 0;
+    if (status & kStatusPairsCapped) rc = AT_E_CAPACITY;  // the first kMaxPairs pairs' detections are kept
     if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow)) {
       rc = AT_E_CAPACITY;
     } else {
@@ -1050,7 +1051,8 @@ int at_set_debug_taps(at_detector* d, int enable) {
 int at_frame_status(at_detector* d, int frame) {
   if (!d || frame < 0 || frame >= d->last_nframes) return AT_E_INVALID;
   const uint32_t s = d->h_ctrl[kCtlStatus * d->B + frame];
-  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow))
+  return (s & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow |
+               kStatusPairsCapped))
              ? AT_E_CAPACITY
              : AT_OK;
 }

@@ -77,6 +77,7 @@ constexpr uint32_t kStatusHashFull = 2u;
 constexpr uint32_t kStatusDetsOverflow = 4u;
 constexpr uint32_t kStatusPointsOverflow = 8u;
 constexpr uint32_t kStatusQuadsOverflow = 16u;
+constexpr uint32_t kStatusPairsCapped = 32u;  // > kMaxPairs pairs: the first kMaxPairs (rank order) processed
 constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config.max_batch)
 // Every kept blob pair can yield one accepted quad and every accepted quad at most
 // one detection, so sizing both queues by kMaxPairs makes neither of them a cap:

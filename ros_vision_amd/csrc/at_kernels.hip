@@ -951,14 +951,13 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   // count and global index (for the segment bases written at the end)
   uint32_t c_slot[kPairsEntCache], c_cnt[kPairsEntCache], c_idx[kPairsEntCache];
   bool c_lds[kPairsEntCache];
-#pragma unroll
-  for (int k = 0; k < kPairsEntCache; k++) { c_slot[k] = 0xffffffffu; c_cnt[k] = 0; c_idx[k] = 0; c_lds[k] = false; }
   __shared__ uint32_t s_tpre[kMaxTilesPerFrame + 1];
   uint32_t tot_e = 0;
+  const int ntb = g.ntb;
+  uint32_t novf = 0;
   {
     // tile entry counts -> exclusive prefix in LDS (one load round trip), then
     // every entry of the frame in one flat pass
-    const int ntb = g.ntb;
     // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
     const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
     const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
@@ -966,33 +965,91 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     if (tid < ntb) s_tpre[tid] = incl_e - ne;
     if (tid == 0) s_tpre[ntb] = tot_e;
     if (np) atomicAdd(&s_np, np);
+    novf = min(b.npent[f], (uint32_t)kPairEntCap);
     __syncthreads();
+  }
+  // entry i of the frame's flat list: (global index, index within its tile)
+  auto entry = [&](uint32_t i, uint32_t* et) -> size_t {
+    int lo = 0, hi = ntb - 1;  // last tile whose prefix <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_tpre[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    *et = i - s_tpre[lo];
+    return ((size_t)f * ntb + lo) * kLdsPairSlots + *et;
+  };
+  // one pass over every entry of the frame, merging the keys below `limit`
+  auto merge_pass = [&](uint64_t limit) {
+#pragma unroll
+    for (int k = 0; k < kPairsEntCache; k++) { c_slot[k] = 0xffffffffu; c_cnt[k] = 0; c_idx[k] = 0; c_lds[k] = false; }
     for (uint32_t i = tid, k = 0; i < tot_e; i += 1024, k++) {
-      int lo = 0, hi = ntb - 1;  // last tile whose prefix <= i
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_tpre[mid] <= i) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t et = i - s_tpre[lo];
-      const size_t e = ((size_t)f * ntb + lo) * kLdsPairSlots + et;
+      uint32_t et;
+      const size_t e = entry(i, &et);
       const uint32_t cnt = b.pent_cnt[e];
-      const uint32_t slot = merge(b.pent_key[e], cnt);
+      const uint64_t key = b.pent_key[e];
+      const uint32_t slot = key < limit ? merge(key, cnt) : 0xffffffffu;
       if (k < (uint32_t)kPairsEntCache) {
 #pragma unroll
         for (int kk = 0; kk < kPairsEntCache; kk++)  // (constant register indices)
           if (kk == (int)k) { c_slot[kk] = slot; c_cnt[kk] = cnt; c_idx[kk] = (uint32_t)e; c_lds[kk] = et < (uint32_t)kGrpEnt; }
-      } else if (et < (uint32_t)kGrpEnt) {
-        b.pent_cnt[e] = kGrpFallback;  // beyond the register cache: k_group reserves per point
       }
     }
-    const uint32_t novf = min(b.npent[f], (uint32_t)kPairEntCap);
-    for (uint32_t i = tid; i < novf; i += 1024) merge(b.povf_key[(size_t)f * kPairEntCap + i], b.povf_cnt[(size_t)f * kPairEntCap + i]);
-    __syncthreads();
-    if (tid == 0) {
-      b.npts[f] = s_np;           // boundary points of the frame (N_c)
-      b.npent[f] = tot_e + novf;  // entries merged (diagnostic)
+    for (uint32_t i = tid; i < novf; i += 1024) {
+      const uint64_t key = b.povf_key[(size_t)f * kPairEntCap + i];
+      if (key < limit) merge(key, b.povf_cnt[(size_t)f * kPairEntCap + i]);
     }
+    __syncthreads();
+  };
+  merge_pass(~0ull);
+  bool capped = false;
+  if (s_full) {
+    // More than kMaxPairs pairs (the 12-bit blob index, points.h:183-193; the
+    // reference overflows its 2048-entry extents buffer here, apriltag_gpu.cu:129,
+    // 899-902): keep exactly the first kMaxPairs pairs in rank order (rep01
+    // ascending) -- the largest limit T below which the frame has at most kMaxPairs
+    // distinct keys, by bisection with the LDS table as the distinct counter --
+    // and flag the frame (kStatusPairsCapped: AT_E_CAPACITY with its detections).
+    capped = true;
+    uint64_t lo = 0, hi = 1ull << 40;  // ok(lo), !ok(hi)
+    while (hi - lo > 1) {
+      const uint64_t mid = lo + ((hi - lo) >> 1);
+      for (int i = tid; i < kHashSlots; i += 1024) { t_key[i] = 0; t_cnt[i] = 0; }
+      if (tid == 0) s_full = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < tot_e; i += 1024) {
+        uint32_t et;
+        const uint64_t key = b.pent_key[entry(i, &et)];
+        if (key < mid && !s_full) merge(key, 1u);
+      }
+      for (uint32_t i = tid; i < novf; i += 1024) {
+        const uint64_t key = b.povf_key[(size_t)f * kPairEntCap + i];
+        if (key < mid && !s_full) merge(key, 1u);
+      }
+      __syncthreads();
+      const bool ok = !s_full;
+      __syncthreads();
+      if (ok) lo = mid;
+      else hi = mid;
+    }
+    for (int i = tid; i < kHashSlots; i += 1024) { t_key[i] = 0; t_cnt[i] = 0; }
+    if (tid == 0) s_full = 0;
+    __syncthreads();
+    merge_pass(lo);
+  }
+  // tile entries beyond the register cache that k_group would look up in LDS:
+  // their points reserve per point (kGrpFallback) -- written after the merge
+  // passes, which read the counts
+  for (uint32_t i = tid + 1024 * kPairsEntCache; i < tot_e; i += 1024) {
+    uint32_t et;
+    const size_t e = entry(i, &et);
+    if (et < (uint32_t)kGrpEnt) b.pent_cnt[e] = kGrpFallback;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    b.npts[f] = s_np;           // boundary points of the frame (N_c)
+    b.npent[f] = tot_e + novf;  // entries merged (diagnostic)
+    if (capped) atomicOr(b.status + f, kStatusPairsCapped);
   }
   __syncthreads();
   stamp(1);
@@ -1116,10 +1173,12 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPairsEntCache; k++) {
-    if (c_slot[k] != 0xffffffffu && c_lds[k]) {
+    if (c_lds[k] && c_slot[k] != 0xffffffffu) {
       const uint32_t tc = t_cnt[c_slot[k]];
       const bool keep = tc >= g.min_cluster && tc <= g.max_cluster;
       b.pent_cnt[c_idx[k]] = keep ? t_off[c_slot[k]] + atomicAdd(&t_cur[c_slot[k]], c_cnt[k]) : kGrpDrop;
+    } else if (c_lds[k]) {
+      b.pent_cnt[c_idx[k]] = kGrpDrop;  // a pair past the first kMaxPairs (capped frame)
     }
   }
   __syncthreads();

@@ -267,14 +267,21 @@ def test_pose_disabled_and_camera_to_robot(gpu):
 
 
 @pytest.mark.parametrize("kind", ["white_noise", "block_noise_8", "block_noise_24", "checker_10",
-                                  "vstripes_2", "diag_4"])
+                                  "vstripes_2", "diag_4", "tags_over_checker"])
 def test_noise_frames(gpu, oracle_mod, kind):
-    """Pathological inputs: pixel noise (blob-pair capacity: both sides report it,
-    the reference overflows its 2048-entry extents buffer, apriltag_gpu.cu:129,899)
-    and blocky noise (thousands of rectangles -> many quads and decodes)."""
+    """Pathological inputs: pixel noise, blocky noise (thousands of rectangles -> many
+    quads and decodes), and more blob pairs than the 12-bit blob index holds
+    (checker_10, tags_over_checker): the reference overflows its 2048-entry extents
+    buffer there (apriltag_gpu.cu:129,899-902, undefined); both sides keep the first
+    4096 pairs in rank order, report AT_E_CAPACITY and return those pairs' detections."""
+    from ros_vision_amd import synth
     rng = np.random.default_rng({"white_noise": 11, "block_noise_8": 12, "block_noise_24": 13, "checker_10": 14,
-                                 "vstripes_2": 15, "diag_4": 16}[kind])
-    if kind == "white_noise":
+                                 "vstripes_2": 15, "diag_4": 16, "tags_over_checker": 17}[kind])
+    if kind == "tags_over_checker":  # tags in the top rows (small labels: first ranks), ~5,000 dark squares below
+        yy, xx = np.mgrid[0:720, 0:1280]
+        frame = np.where(((yy % 12) < 10) & ((xx % 12) < 10), 25, 230).astype(np.uint8)
+        frame[:200] = synth.render_board(1280, 200, seed=17, ntags=5, side_range=(70, 90))[0]
+    elif kind == "white_noise":
         frame = rng.integers(0, 256, size=(720, 1280), dtype=np.uint8)
     elif kind == "checker_10":  # > 4096 blob pairs of >= 25 pixels
         yy, xx = np.mgrid[0:720, 0:1280]
@@ -294,10 +301,12 @@ def test_noise_frames(gpu, oracle_mod, kind):
     orc = oracle_mod.Oracle(1280, 720)
     rc = orc.detect(frame, 2)
     from ros_vision_amd.detector import AT_E_CAPACITY
-    if orc.status() == AT_E_CAPACITY:
-        assert det.frame_status(0) == AT_E_CAPACITY and dets == []
-        return
-    assert rc >= 0 and det.frame_status(0) >= 0
+    if kind in ("checker_10", "tags_over_checker"):
+        assert orc.status() == AT_E_CAPACITY and orc.num_pairs() == 4096
+    assert det.frame_status(0) == orc.status()
+    if kind == "tags_over_checker":
+        assert [d.id for d in dets] == [434, 435, 436, 437, 438]  # the tags' pairs rank first (smallest labels)
+    assert rc >= 0
     assert compare_frame(det, orc) == []
     assert compare_detections(dets, orc.detections()) == []
 

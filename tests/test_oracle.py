@@ -207,3 +207,22 @@ def test_cpu_oracle_stage_invariants(oracle_mod):
     # index points sorted by (blob, theta) (P6)
     ip = o.sorted_index_points() >> np.uint64(24)
     assert np.all(np.diff(ip.astype(np.int64)) >= 0)
+
+
+def test_pair_capacity_keeps_the_first_4096_pairs(oracle_mod):
+    """More blob pairs than the 12-bit blob index holds (points.h:183-193; the
+    reference overflows its 2048-entry extents buffer, apriltag_gpu.cu:129,899-902):
+    the first 4096 pairs in P2 rank order are processed, the rest dropped, the status
+    is AT_E_CAPACITY and the kept pairs' tags are still detected."""
+    from ros_vision_amd import synth
+    codes = dict(oracle_mod.family_entries())
+    yy, xx = np.mgrid[0:720, 0:1280]
+    frame = np.where(((yy % 12) < 10) & ((xx % 12) < 10), 25, 230).astype(np.uint8)  # ~5,000 dark squares
+    frame[:200] = synth.render_board(1280, 200, seed=17, ntags=5, side_range=(70, 90), codes=codes)[0]
+    o = oracle_mod.Oracle(1280, 720)
+    o.detect(frame, 2)
+    assert o.status() == -3 and o.num_pairs() == 4096
+    assert [d["id"] for d in o.detections()] == [434, 435, 436, 437, 438]
+    ip = o.sorted_index_points()
+    assert ip.size and int(ip.max() >> 52) <= 4095  # blob indices of the kept pairs only
+    assert len(o.quads()) > 3000  # the kept squares still go through quad fitting
