@@ -55,6 +55,12 @@ def parse():
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP default 4): one hardware queue per "
                          "detector stream so the batches in flight run concurrently")
+    ap.add_argument("--host-ingest-steps", type=int, default=20,
+                    help="steps of the same loop fed from page-locked host frames (at_enqueue_host: H2D on the "
+                         "detector streams), reported as host_ingest; 0 = skip")
+    ap.add_argument("--c3-latency-iters", type=int, default=300,
+                    help="config C3 latency: one batch of 4 camera frames (pageable host memory) -> detections, "
+                         "p50 over this many batches; 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
     ap.add_argument("--timed-kernel", default=None,
@@ -78,10 +84,10 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
         return nf * (2 * W * H + W * H + Wd * Hd)           # YUYV in, gray + decimated out
     if kernel == "k_boundary":
         return nf * 5 * Wd * Hd + 8 * stats.get("boundary_points", 0)  # thr + labels in, points out
-    if kernel == "k_blob":  # kept blobs: 8-B sort key in + 4 gradient bytes per point
-        return 12 * stats.get("large_blob_points", 0)
+    if kernel == "k_blob":  # kept blobs: the 8-B sort key of every point (the line-fit weight W rides in it)
+        return 8 * stats.get("large_blob_points", 0)
     if kernel == "k_blob_small":
-        return 12 * stats.get("small_blob_points", 0)
+        return 8 * stats.get("small_blob_points", 0)
     if kernel == "k_extents":  # candidate points read (bounded by all boundary points), kept points' keys written
         return 8 * stats.get("boundary_points", 0) + 8 * (stats.get("small_blob_points", 0) +
                                                           stats.get("large_blob_points", 0))
@@ -202,7 +208,7 @@ def main():
             root_pool = torch.empty((world, npool) + frames.shape[1:], dtype=torch.uint8, device="cuda")
             for r in range(world):
                 root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames)
-        ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda")
+        ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
         rec_cap = 32  # detection records per frame gathered to rank 0 (fixed capacity)
         rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)
         send = [torch.empty((B, rec_bytes + 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
@@ -238,27 +244,34 @@ def main():
         return runner.run(nsteps, step0)
 
     def run_scatter(nsteps, step0):
-        """Scatter of step k+1 overlaps detection of step k (double-buffered)."""
+        """The scatter of step k+1 overlaps the detection of steps k-instances+2 .. k:
+        the same in-flight depth as the local-ingest loop (one frame buffer per
+        instance; a buffer is rescattered only after the batch that read it is
+        collected)."""
         ndet = 0
-        prev = None
+        ni = len(dets)
+        inflight = []
+
+        def drain():
+            pd, ps = inflight.pop(0)
+            if id(pd) in copied:  # its pinned buffer may still be copied from
+                copied[id(pd)].synchronize()
+            n = sum(pd.collect(counts_only=True))
+            gather_results(pd, ps)
+            return n
+
         ingest.start(step0)
-        for s in range(nsteps):
-            d = dets[s % 2]
-            buf = ingest.ready(step0 + s, detector=d)  # stream dependency, no host wait
+        for s in range(step0, step0 + nsteps):
+            d = dets[(s - step0) % ni]
+            buf = ingest.ready(s, detector=d)  # stream dependency, no host wait
             d.enqueue_device(buf.data_ptr(), stride, B)
-            if prev is not None:
-                if id(prev) in copied:  # its pinned buffer may still be copied from
-                    copied[id(prev)].synchronize()
-                ndet += sum(prev.collect(counts_only=True))
-                gather_results(prev, step0 + s - 1)
-            prev = d
-            if s + 1 < nsteps:
-                ingest.start(step0 + s + 1)  # its buffer was read by step s-1, collected above
-        if prev is not None:
-            if id(prev) in copied:
-                copied[id(prev)].synchronize()
-            ndet += sum(prev.collect(counts_only=True))
-            gather_results(prev, step0 + nsteps - 1)
+            inflight.append((d, s))
+            if len(inflight) == ni:
+                ndet += drain()
+            if s + 1 < step0 + nsteps:
+                ingest.start(s + 1)  # its buffer was read by step s+1-instances, collected above
+        while inflight:
+            ndet += drain()
         for w in gwork:
             if w is not None:
                 w.wait()
@@ -335,6 +348,44 @@ def main():
     lat_h = np.array(lat_h or [0.0]) * 1e3
     lat_d = np.array(lat_d or [0.0]) * 1e3
 
+    # config C3 (4 cameras, one batch per launch sequence): 4 host frames -> detections
+    lat_c3 = []
+    if args.c3_latency_iters > 0:
+        c3 = rva.GpuDetector(W, H, max_batch=4, device=local_rank)
+        cams = [np.ascontiguousarray(frames[(7 * c) % args.pool]) for c in range(4)]
+        for i in range(10):
+            c3.detect_batch(cams)
+        for i in range(args.c3_latency_iters):
+            t1 = time.perf_counter()
+            c3.detect_batch(cams)
+            lat_c3.append(time.perf_counter() - t1)
+        c3.close()
+    lat_c3 = np.array(lat_c3 or [0.0]) * 1e3
+
+    # the same loop fed from page-locked host frames: what a camera-fed GPU sustains
+    host_ingest = None
+    if args.host_ingest_steps > 0 and not scatter:
+        pinned = torch.from_numpy(frames).pin_memory()
+        hrun = StreamRunner(dets, pinned.data_ptr(), stride, args.pool, B, host=True)
+        hrun.run(len(dets))
+        torch.cuda.synchronize()
+        if dist.is_initialized():
+            dist.barrier()
+        t1 = time.perf_counter()
+        hrun.run(args.host_ingest_steps)
+        torch.cuda.synchronize()
+        h_el = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([h_el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            h_el = float(t.item())
+        h_fps = world * args.host_ingest_steps * B / h_el
+        host_ingest = {"value": round(h_fps, 2), "unit": "frames/s", "steps": args.host_ingest_steps,
+                       "h2d_GBps_per_gpu": round(h_fps / world * stride / 1e9, 2),
+                       "note": "frames in page-locked host memory, copied H2D on the detector streams "
+                               "(at_enqueue_host) while other batches compute; bounded by the host-to-device link"}
+        del pinned
+
     if rank != 0:
         if dist.is_initialized():
             dist.barrier()
@@ -365,8 +416,11 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": "configs[1]: 1280x720 single-camera synthetic tag36h11 stream "
-                               "(%d tags/frame, YUYV, frames resident in HBM)" % args.tags,
+        "config": {"workload": ("configs[1]: 1280x720 single-camera synthetic tag36h11 stream "
+                                "(%d tags/frame, YUYV, frames resident in HBM)" % args.tags)
+                               if (W, H) == (1280, 720) else
+                               ("configs[3] geometry: %dx%d synthetic tag36h11 frames (%d tags/frame, YUYV, "
+                                "frames resident in HBM), one GPU" % (W, H, args.tags)),
                    "width": W, "height": H, "batch_per_gpu": B, "distinct_frames_per_gpu": args.pool,
                    "frames_resident_per_gpu": npool,
                    "parallelism": ("frame-sharded x%d, frames scattered from rank 0 over RCCL, records gathered "
@@ -378,6 +432,10 @@ def main():
         "latency_note": "B=1, pageable host YUYV frame -> detections + poses in host memory",
         "p50_latency_hbm_ms": round(float(np.percentile(lat_d, 50)), 4),
         "p99_latency_hbm_ms": round(float(np.percentile(lat_d, 99)), 4),
+        "p50_latency_c3_ms": round(float(np.percentile(lat_c3, 50)), 4),
+        "p99_latency_c3_ms": round(float(np.percentile(lat_c3, 99)), 4),
+        "latency_c3_note": "config C3: one batch of 4 camera frames (pageable host YUYV) -> detections + poses",
+        "host_ingest": host_ingest,
         "detections_per_frame": round(ndet / total_frames, 3),
         "roofline": {"bound": "hbm", "kernel": dominant,
                      "achieved": round(k_achieved, 3) if k_achieved else None, "peak": HBM_PEAK_GBS,

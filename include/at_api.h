@@ -103,6 +103,13 @@ int at_detect_device(at_detector *d, const void *d_frames, size_t frame_stride, 
  * runs the host tail (reconcile + sort by id). */
 int at_enqueue_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt);
 int at_collect(at_detector *d, at_detection *out, int cap_per_frame, int *n_per_frame);
+/* Split-phase form of at_detect_batch (camera-fed pipelines): the host-to-device
+ * copies of the frames (one per run of back-to-back frames; page-locked sources,
+ * e.g. hipHostMalloc'd or registered, copy asynchronously) and the batch are
+ * enqueued on the detector's stream, so with several detectors in turn the copies
+ * of one batch overlap the kernels of another.  The frames must stay untouched
+ * until at_collect. */
+int at_enqueue_host(at_detector *d, const uint8_t *const *frames, int nframes, at_pixfmt fmt);
 
 /* Stream ordering without a host wait: the detector's next enqueued batch starts
  * only after everything queued so far on `stream` (a hipStream_t of the same

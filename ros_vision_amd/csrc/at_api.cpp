@@ -725,19 +725,36 @@ static size_t frame_bytes(const at_detector* d, int fmt) {
 
 extern "C" {
 
-int at_detect_batch(at_detector* d, const uint8_t* const* frames, int nframes, at_pixfmt fmt, at_detection* out,
-                    int cap_per_frame, int* n_per_frame) {
+int at_enqueue_host(at_detector* d, const uint8_t* const* frames, int nframes, at_pixfmt fmt) {
   if (!d || !frames || nframes < 1 || nframes > d->B || !check_fmt(fmt)) return AT_E_INVALID;
+  for (int f = 0; f < nframes; f++)
+    if (!frames[f]) return AT_E_INVALID;
   HIPCHK(hipSetDevice(d->device));
   if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));  // the frame table is read by the pending batch
   const size_t fb = frame_bytes(d, fmt);
-  for (int f = 0; f < nframes; f++) {
-    HIPCHK(hipMemcpyAsync(d->d_in + (size_t)f * d->in_stride, frames[f], fb, hipMemcpyHostToDevice, d->st));
-    d->h_ftab[f] = d->d_in + (size_t)f * d->in_stride;
+  // frames back to back in host memory go over in one copy (their staging slots
+  // are in_stride apart: one 2-D copy)
+  for (int f = 0; f < nframes;) {
+    int r = 1;
+    while (f + r < nframes && frames[f + r] == frames[f] + (size_t)r * fb) r++;
+    uint8_t* dst = d->d_in + (size_t)f * d->in_stride;
+    if (r == 1)
+      HIPCHK(hipMemcpyAsync(dst, frames[f], fb, hipMemcpyHostToDevice, d->st));
+    else
+      HIPCHK(hipMemcpy2DAsync(dst, d->in_stride, frames[f], fb, fb, (size_t)r, hipMemcpyHostToDevice, d->st));
+    for (int k = 0; k < r; k++) d->h_ftab[f + k] = d->d_in + (size_t)(f + k) * d->in_stride;
+    f += r;
   }
-  int rc = enqueue(d, nframes, fmt);
+  const int rc = enqueue(d, nframes, fmt);
   if (rc) return rc;
   d->last_staged = 1;
+  return AT_OK;
+}
+
+int at_detect_batch(at_detector* d, const uint8_t* const* frames, int nframes, at_pixfmt fmt, at_detection* out,
+                    int cap_per_frame, int* n_per_frame) {
+  const int rc = at_enqueue_host(d, frames, nframes, fmt);
+  if (rc) return rc;
   return collect(d, out, cap_per_frame, n_per_frame);
 }
 

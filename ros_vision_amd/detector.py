@@ -33,7 +33,7 @@ EXPORTS = [
     "at_set_profiling", "at_stage_times", "at_stage_name", "at_poses", "at_tag_detections",
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
     "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
-    "at_draw_outlines_device", "at_detections", "at_max_detections", "at_annotate_staged",
+    "at_draw_outlines_device", "at_detections", "at_max_detections", "at_annotate_staged", "at_enqueue_host",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -158,6 +158,8 @@ def load_library(path: str = LIB_PATH):
     L.at_detect_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(AtDetection),
                                    C.c_int, C.POINTER(C.c_int)]
     L.at_enqueue_device.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]
+    if hasattr(L, "at_enqueue_host"):
+        L.at_enqueue_host.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int]
     L.at_collect.argtypes = [C.c_void_p, C.POINTER(AtDetection), C.c_int, C.POINTER(C.c_int)]
     L.at_stream_wait.argtypes = [C.c_void_p, C.c_void_p]
     L.at_frame_status.argtypes = [C.c_void_p, C.c_int]
@@ -362,6 +364,13 @@ class GpuDetector:
         _check(load_library().at_enqueue_device(self._h, C.c_void_p(dev_ptr), frame_stride, nframes, fmt),
                "at_enqueue_device")
         self._pending = nframes
+
+    def enqueue_host(self, host_ptrs, fmt: int = AT_FMT_YUYV):
+        """at_enqueue_host: host frames (addresses; page-locked for an asynchronous
+        copy) copied and detected on this detector's stream; collect() later."""
+        ptrs = (C.c_void_p * len(host_ptrs))(*host_ptrs)
+        _check(load_library().at_enqueue_host(self._h, ptrs, len(host_ptrs), fmt), "at_enqueue_host")
+        self._pending = len(host_ptrs)
 
     def wait_stream(self, stream_handle: int):
         """at_stream_wait: the next enqueued batch waits (on the GPU) for the work queued

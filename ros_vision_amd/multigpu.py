@@ -75,23 +75,26 @@ def gather_detections(dist, packed: np.ndarray, device):
 
 
 class ScatterIngest:
-    """Double-buffered frame ingest from rank 0 (north-star topology).
+    """Multi-buffered frame ingest from rank 0 (north-star topology).
 
     Rank 0 holds every rank's frames in device memory; ``start(step)`` launches
     the scatter of step `step`'s batch (async RCCL/gloo collective) into buffer
-    step % 2, ``ready(step)`` waits for it and returns that buffer.  The caller
-    must have finished reading buffer (step % 2) -- i.e. collected step - 2 --
-    before ``start(step)``.
+    step % nbuf, ``ready(step)`` waits for it and returns that buffer.  The caller
+    must have finished reading buffer (step % nbuf) -- i.e. collected step - nbuf --
+    before ``start(step)``; nbuf = the batches in flight keeps the same depth as
+    the local-ingest pipeline.
     """
 
-    def __init__(self, dist, root_pool, batch: int, frame_shape, device):
+    def __init__(self, dist, root_pool, batch: int, frame_shape, device, nbuf: int = 2):
         import torch
         self.dist, self.batch, self.device = dist, batch, device
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         self.pool = root_pool  # rank 0: [world, npool, *frame_shape] (None elsewhere)
         self.npool = int(root_pool.shape[1]) if root_pool is not None else 0
-        self.buf = [torch.empty((batch,) + tuple(frame_shape), dtype=torch.uint8, device=device) for _ in range(2)]
-        self.work = [None, None]
+        self.nbuf = max(2, int(nbuf))
+        self.buf = [torch.empty((batch,) + tuple(frame_shape), dtype=torch.uint8, device=device)
+                    for _ in range(self.nbuf)]
+        self.work = [None] * self.nbuf
 
     def _chunks(self, step):
         if self.rank != 0:
@@ -102,7 +105,7 @@ class ScatterIngest:
         return [self.pool[r, off:off + self.batch] for r in range(self.world)]
 
     def start(self, step):
-        i = step % 2
+        i = step % self.nbuf
         self.work[i] = self.dist.scatter(self.buf[i], scatter_list=self._chunks(step), src=0, async_op=True)
 
     def ready(self, step, detector=None):
@@ -110,7 +113,7 @@ class ScatterIngest:
         `detector`'s stream as a stream dependency (at_stream_wait), not a host wait;
         without a detector the host synchronizes torch's stream."""
         import torch
-        i = step % 2
+        i = step % self.nbuf
         self.work[i].wait()  # torch's current stream now waits for the collective
         if self.buf[i].is_cuda:
             stream = torch.cuda.current_stream(self.buf[i].device)

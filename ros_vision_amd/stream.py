@@ -35,13 +35,27 @@ class StreamRunner:
     frames in it.  Step s reads the `batch` frames at offset
     ``offset(s)`` (consecutive batches walk the pool and wrap)."""
 
-    def __init__(self, detectors, base: int, stride: int, npool: int, batch: int, fmt: int = AT_FMT_YUYV):
+    def __init__(self, detectors, base: int, stride: int, npool: int, batch: int, fmt: int = AT_FMT_YUYV,
+                 host: bool = False):
+        """host=True: `base` is a host (page-locked) pool and the frames go through
+        at_enqueue_host (H2D copies on the detector's stream); a batch may then be
+        larger than the pool (frames taken modulo the pool)."""
         self.dets = list(detectors)
         self.base, self.stride, self.npool, self.batch, self.fmt = base, stride, npool, batch, fmt
+        self.host = host
 
     def offset(self, step: int) -> int:
         off = (step * self.batch) % self.npool
+        if self.host:
+            return off
         return 0 if off + self.batch > self.npool else off
+
+    def _enqueue(self, d, step):
+        off = self.offset(step)
+        if self.host:
+            d.enqueue_host([self.base + ((off + j) % self.npool) * self.stride for j in range(self.batch)], self.fmt)
+        else:
+            d.enqueue_device(self.base + off * self.stride, self.stride, self.batch, self.fmt)
 
     def run(self, nsteps: int, step0: int = 0, on_batch=None) -> int:
         """Runs nsteps batches; returns the number of detections.  on_batch(det,
@@ -60,7 +74,7 @@ class StreamRunner:
 
         for s in range(step0, step0 + nsteps):
             d = self.dets[(s - step0) % ni]
-            d.enqueue_device(self.base + self.offset(s) * self.stride, self.stride, self.batch, self.fmt)
+            self._enqueue(d, s)
             inflight.append((d, s))
             if len(inflight) == ni:
                 ndet += drain()

@@ -96,3 +96,28 @@ def test_c4_1080p_throughput_mode(oracle_mod):
         orc.detect(frames[f], 0)
         assert compare_frame(det, orc, frame_idx=f) == []
         assert compare_detections(res[f], orc.detections()) == []
+
+
+def test_host_ingest_loop(c2):
+    """bench.py's host_ingest leg: the same round-robin loop fed from page-locked
+    host frames through at_enqueue_host (H2D copies on the detector streams, runs of
+    back-to-back frames in one 2-D copy, batches wrapping the pool)."""
+    import torch
+
+    import ros_vision_amd as rva
+    from ros_vision_amd.stream import StreamRunner
+    g, frames = c2
+    pinned = torch.from_numpy(frames).pin_memory()
+    B = 48  # batches wrap the 64-frame pool: two copy runs per batch
+    dets = [rva.GpuDetector(1280, 720, max_batch=B) for _ in range(3)]
+    runner = StreamRunner(dets, pinned.data_ptr(), frames[0].nbytes, frames.shape[0], B, host=True)
+    bad, seen = [], []
+
+    def check(det, step, off):
+        res = det.results()
+        for j in range(B):
+            bad.extend(compare_with_stream_golden(g, (off + j) % frames.shape[0], res[j], det.poses(j)))
+        seen.append(step)
+
+    runner.run(5, 0, on_batch=check)
+    assert bad == [] and seen == [0, 1, 2, 3, 4]
