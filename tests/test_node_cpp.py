@@ -401,3 +401,14 @@ def test_mock_node_from_camera_serial_1080p(built, oracle_mod, tmp_path, nodelib
     nodelib.at_node_draw_detection_outlines(cpu.ctypes.data, W, H, dets, len(want))
     gpu_img = np.fromfile(img_out, np.uint8).reshape(H, W, 3)
     assert not np.array_equal(cpu, bgr) and np.array_equal(gpu_img, cpu)
+
+
+def test_ros2_node_type_checks():
+    """node/ros2_apriltags_node.cpp (the rclcpp binding; ROS 2 is absent here) compiles
+    against type-check stand-ins of the rclcpp / sensor_msgs / ament_index API it uses
+    and the reference's message layouts (msg/TagDetection.msg: int32 id, float64 x y z)."""
+    stub = os.path.join(ROOT, "tests", "ros_stub")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I" + stub,
+                        "-I" + NODE, os.path.join(NODE, "ros2_apriltags_node.cpp")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
