@@ -266,6 +266,13 @@ __device__ __forceinline__ uint32_t slot_of(int ty, int tx, int type) {
   return (uint32_t)(ty * T::ROW_NODES + (type == 0 ? tx : T::BW + 2 * tx + (type - 1)));
 }
 
+// kept bit of a root's parent word: the component has >= 25 pixels (BlobDiff's
+// size test, apriltag_gpu.cu:331-337), throughput mode
+constexpr uint32_t kKeptBit = 0x80000000u;
+// s_cnt flag of a local root whose component reaches a border block of the tile
+// (only those can take part in k_ccl_border's unions)
+constexpr uint32_t kTouchBit = 0x80000000u;
+
 template <int TWD>
 __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
@@ -430,6 +437,13 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   if (nfg) atomicAdd(&s_cnt[rF], nfg);
   if (nbl) atomicAdd(&s_cnt[rL], nbl);
   if (nbr) atomicAdd(&s_cnt[rR], nbr);
+  // components reaching a border block may be merged across tiles (k_ccl_border);
+  // every other component is complete here: root and pixel count are final
+  if (bty == 0 || bty == CT::BH - 1 || btx == 0 || btx == kCclBW - 1) {
+    if (nfg) atomicOr(&s_cnt[rF], kTouchBit);
+    if (nbl) atomicOr(&s_cnt[rL], kTouchBit);
+    if (nbr) atomicOr(&s_cnt[rR], kTouchBit);
+  }
   __syncthreads();
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
@@ -445,24 +459,32 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
     const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
     const uint32_t idL = idF + g.Wd;
-    *reinterpret_cast<uint2*>(par + idF) = make_uint2(gid(rF), idF + 1);
-    *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL), gid(rR));
     // sizes only at local roots with pixels: every other entry is never read
     // (k_boundary reads component roots, k_ccl_roots the listed local roots; the
     // AT_STAGE_SIZES tap masks the plane with the forest, k_tap_sizes)
-    const uint32_t cF = rF == F ? s_cnt[F] : 0u, cL = rL == L ? s_cnt[L] : 0u, cR = rR == R ? s_cnt[R] : 0u;
+    const uint32_t wF = rF == F ? s_cnt[F] : 0u, wL = rL == L ? s_cnt[L] : 0u, wR = rR == R ? s_cnt[R] : 0u;
+    const uint32_t cF = wF & ~kTouchBit, cL = wL & ~kTouchBit, cR = wR & ~kTouchBit;
+    // a root of a tile-interior component is final: in throughput mode (k_ccl_keep
+    // follows) its parent word gets the kept bit here and it is not listed
+    constexpr bool kKeep = TWD != 32;
+    auto fin = [&](uint32_t w, uint32_t c) -> uint32_t {
+      return (kKeep && c && !(w & kTouchBit) && c >= 25) ? kKeptBit : 0u;
+    };
+    *reinterpret_cast<uint2*>(par + idF) = make_uint2(gid(rF) | fin(wF, cF), idF + 1);
+    *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL) | fin(wL, cL), gid(rR) | fin(wR, cR));
     if (cF) size[idF] = cF;
     if (cL | cR) {
       if (cL && cR) *reinterpret_cast<uint2*>(size + idL) = make_uint2(cL, cR);
       else if (cL) size[idL] = cL;
       else size[idL + 1] = cR;
     }
-    // the tile's local roots (components with pixels), for k_ccl_roots
+    // the tile's local roots of components reaching its border (with pixels), for
+    // k_ccl_roots / k_ccl_keep
     const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
     uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-    if (cF) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
-    if (cL) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
-    if (cR) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
+    if (cF && (wF & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
+    if (cL && (wL & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
+    if (cR && (wR & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
   if (tid == 0) b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
@@ -619,8 +641,8 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
 // Once every count has reached its root: each local root's parent word becomes
 // root | kept << 31 (kept: the component has >= 25 pixels, the BlobDiff size
 // test, apriltag_gpu.cu:331-337), so k_boundary reads label and size test in the
-// same two hops and never touches the size plane.
-constexpr uint32_t kKeptBit = 0x80000000u;
+// same two hops and never touches the size plane.  (Roots of components inside
+// one CCL tile got theirs from k_thr_ccl already and are not listed.)
 __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
   const int f = blockIdx.y;
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
