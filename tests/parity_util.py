@@ -33,8 +33,14 @@ def compare_frame(det, orc, frame_idx=0, check_points=True):
     oqi = [(int(f.blob_index), tuple(int(v) for v in f.indices)) for f in oq]
     if gqi != oqi:
         bad.append("valid fit quads differ: %s vs %s" % (gqi[:5], oqi[:5]))
-    ga = [(q["blob_index"], q["corners"].tobytes()) for q in det.copy_quads(frame_idx) if q["accepted"]]
-    oa = [(b, c.tobytes()) for c, b in orc.quads()]
+    # corners bit for bit; a NaN corner (a degenerate line fit: both sides accept the
+    # quad, UpdateFitQuads' area test is false on NaN) compares by NaN-ness, not by
+    # its payload (the GPU's default NaN is positive, x86's negative)
+    def canon(c):
+        c = np.asarray(c, np.float32)
+        return np.where(np.isnan(c), np.float32(np.nan), c).tobytes()
+    ga = [(q["blob_index"], canon(q["corners"])) for q in det.copy_quads(frame_idx) if q["accepted"]]
+    oa = [(b, canon(c)) for c, b in orc.quads()]
     if ga != oa:
         bad.append("accepted quad corners differ (%d vs %d)" % (len(ga), len(oa)))
     return bad
