@@ -314,7 +314,14 @@ def main():
     host1 = [d.batch_stats() for d in dets]
     kt = [d.kernel_time() for d in dets] if ktimer else [(0.0, 0)]
     k_launches = sum(n for _, n in kt)
-    k_ms = sum(ms * n for ms, n in kt) / max(1, k_launches)
+    k_ms_events = sum(ms * n for ms, n in kt) / max(1, k_launches)
+    ks = [d.kernel_span() for d in dets] if ktimer else [(0.0, 0)]
+    k_spans = sum(n for _, n in ks)
+    k_ms_span = sum(ms * n for ms, n in ks) / max(1, k_spans)
+    # the kernel's execution span on the device clock (what rocprofv3's kernel trace
+    # reports); the HIP-event bracket also holds the launch's wait for free CUs
+    # behind the other batches in flight
+    k_ms = k_ms_span if k_spans else k_ms_events
     stats = dets[0].batch_stats()
     for d in dets:
         d.set_kernel_timer(None)
@@ -442,9 +449,17 @@ def main():
                      "unit": "GB/s", "frac": round(k_achieved / HBM_PEAK_GBS, 6) if k_achieved else None,
                      "traffic": k_traffic, "algorithmic_bytes_per_launch": kbytes,
                      "avg_launch_ms": round(k_ms, 5), "launches_timed": k_launches,
-                     "note": "dominant kernel by stage time; HIP events around it on its stream in the timed "
-                             "region; algorithmic bytes per DESIGN.md section 4; traffic = PMC "
-                             "(2*FETCH_SIZE+WRITE_SIZE) per launch from profiles/pmc_traffic.json"},
+                     "avg_launch_ms_device_clock": round(k_ms_span, 5), "launches_device_clock": k_spans,
+                     "avg_launch_ms_hip_events": round(k_ms_events, 5),
+                     "frac_hip_events": round(kbytes / (k_ms_events * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+                     if (kbytes and k_ms_events > 0) else None,
+                     "note": "dominant kernel by stage time, timed in the timed region on every launch: "
+                             "avg_launch_ms = its execution span on the device wall clock (first workgroup "
+                             "start to last workgroup end, at_kernel_span; what rocprofv3 --kernel-trace "
+                             "reports), avg_launch_ms_hip_events = HIP events around it on its stream (adds "
+                             "the launch's wait for CUs behind the other batches in flight); algorithmic "
+                             "bytes per DESIGN.md section 4; traffic = PMC (2*FETCH_SIZE+WRITE_SIZE) per "
+                             "launch from profiles/pmc_traffic.json"},
         "roofline_pipeline": {"bound": "hbm", "achieved": round(per_gpu_fps * pipe_bytes / 1e9, 3),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(per_gpu_fps * pipe_bytes / 1e9 / HBM_PEAK_GBS, 6),

@@ -171,6 +171,13 @@ const char *at_stage_name(int stage);
  * at_kernel_time: mean ms per launch and number of launches since set. */
 int at_set_kernel_timer(at_detector *d, int stage);
 int at_kernel_time(at_detector *d, double *avg_ms, long long *launches);
+/* The same launches timed on the device: first workgroup's start to last
+ * workgroup's end on the GPU wall clock (the kernel's execution span, as a
+ * rocprofv3 kernel trace measures it; the HIP events of at_kernel_time also
+ * hold the time the launch waits on the stream for free compute units).
+ * Stamped by k_thr_ccl, k_ccl_border, k_boundary, k_extents, k_blob_small,
+ * k_blob and k_decode; 0 launches for the other stages. */
+int at_kernel_span(at_detector *d, double *avg_ms, long long *launches);
 
 /* Work counts of the last collected batch: [0] frames, [1] boundary points,
  * [2] blob pairs, [3] points processed by the small-blob kernel, [4] by the

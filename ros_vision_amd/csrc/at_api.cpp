@@ -135,6 +135,10 @@ struct at_detector {
   const uint8_t** h_ftab;   // frame pointer table (mapped, fine-grained host memory; k_pre reads it)
   uint32_t* d_ctrl;         // control block (zeroed each batch)
   size_t ctrl_words;
+  size_t kstamp_word;       // first of the timed kernel's stamp words in the control block
+  double wclk_khz;          // device wall clock (s_memrealtime) rate
+  double kd_ms;             // device-clock spans of the timed kernel (sum) and their count
+  long long kd_n;
   uint32_t* h_ctrl;         // pinned copy of the control block
   DevDetection* h_dets;     // pinned [det_cap]: the batch-wide candidate pool (mapped)
   // results of the last collected batch: frame f's detections are the pool records
@@ -349,6 +353,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
     return fail(AT_E_HIP);
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device);
+  int wclk = 0;
+  (void)hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, d->device);
+  d->wclk_khz = wclk > 0 ? (double)wclk : 100000.0;  // s_memrealtime: 100 MHz
   d->nblobwg = std::max(64, ncu * 2);
   if (getenv("AT_BLOB_WG")) d->nblobwg = std::max(16, atoi(getenv("AT_BLOB_WG")));  // experiment: persistent grid size
 
@@ -400,7 +407,10 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.det_cap = (uint32_t)std::max<size_t>(kMaxDets, (size_t)kDetPoolPerFrame * B);
   b.dets = (DevDetection*)dalloc(b.det_cap * sizeof(DevDetection));
   b.quads = (QuadRecord*)dalloc(B * kMaxPairs * sizeof(QuadRecord));
-  d->ctrl_words = kCtlPerFrame * B + kCtlScalars;
+  // control block: per-frame words, scalars, then (8-byte aligned) the timed
+  // kernel's two wall-clock stamps and its finished-workgroup count
+  d->kstamp_word = (kCtlPerFrame * B + kCtlScalars + 1) & ~(size_t)1;
+  d->ctrl_words = d->kstamp_word + 5;
   d->d_ctrl = (uint32_t*)dalloc(((d->ctrl_words * 4 + 15) / 16) * 16);
   b.npts = d->d_ctrl + kCtlNpts * B;
   b.npairs = d->d_ctrl + kCtlNpairs * B;
@@ -416,6 +426,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.blob_pts = sc + kCtlBlobPts;
   b.ncls = sc + kCtlNcls;
   b.det_head = sc + kCtlDetHead;
+  b.kt_stage = -1;
+  b.kstamp = reinterpret_cast<uint64_t*>(d->d_ctrl + d->kstamp_word);
+  b.kdone = d->d_ctrl + d->kstamp_word + 4;
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)
@@ -552,8 +565,9 @@ static int host_tail(const DevDetection* cand, int* idx, int ncand, at_detection
 static hipError_t record_sequence(at_detector* d, int nframes, int fmt, hipStream_t st, hipEvent_t* ev,
                                   const KernelTimer* kt) {
   hipError_t e;
-  if ((e = launch_pipeline(d->d, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join,
-                           kt)))
+  DevBufs b = d->d;
+  b.kt_stage = kt ? kt->stage : -1;  // the timed kernel stamps its device-clock span
+  if ((e = launch_pipeline(b, d->g, d->prm, nframes, fmt, d->nblobwg, st, ev, d->st2, d->ev_fork, d->ev_join, kt)))
     return e;
   // results reach the host zero-copy: k_decode writes the detections into the
   // mapped host buffer and k_pose adds the poses and the control block; without
@@ -682,6 +696,12 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
     HIPCHK(hipEventElapsedTime(&ms, d->kt.t0, d->kt.t1));
     d->kt_ms += ms;
     d->kt_n++;
+    uint64_t st[2];
+    memcpy(st, d->h_ctrl + d->kstamp_word, sizeof(st));
+    if (st[1] > st[0] && st[0] && d->wclk_khz > 0) {  // (kernels without stamps leave zeros)
+      d->kd_ms += (double)(st[1] - st[0]) / d->wclk_khz;
+      d->kd_n++;
+    }
   }
   const int B = d->B;
   int rc = AT_OK;
@@ -831,6 +851,8 @@ int at_set_kernel_timer(at_detector* d, int stage) {
   d->kt.stage = stage;
   d->kt_ms = 0;
   d->kt_n = 0;
+  d->kd_ms = 0;
+  d->kd_n = 0;
   return AT_OK;
 }
 
@@ -838,6 +860,13 @@ int at_kernel_time(at_detector* d, double* avg_ms, long long* launches) {
   if (!d || !avg_ms) return AT_E_INVALID;
   *avg_ms = d->kt_n ? d->kt_ms / (double)d->kt_n : 0.0;
   if (launches) *launches = d->kt_n;
+  return AT_OK;
+}
+
+int at_kernel_span(at_detector* d, double* avg_ms, long long* launches) {
+  if (!d || !avg_ms) return AT_E_INVALID;
+  *avg_ms = d->kd_n ? d->kd_ms / (double)d->kd_n : 0.0;
+  if (launches) *launches = d->kd_n;
   return AT_OK;
 }
 

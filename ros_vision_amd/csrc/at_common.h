@@ -254,6 +254,13 @@ struct DevBufs {
   const uint64_t* book_code;  // [fam.ncodes] codebook (3.x bit order)
   const int32_t* book_id;     // [fam.ncodes] tag id of each code
   float* gp_out;              // [B][gp_c][gp_h][gp_w] game-piece network input (at_gp_enable)
+  // device-clock span of the timed kernel (bench roofline): the stage it is
+  // (-1: none, set in the split graph's copy of DevBufs only), the control-block
+  // words of its first workgroup's start / last workgroup's end (wall clock) and
+  // the count of finished workgroups that finds the last one
+  int32_t kt_stage;
+  uint64_t* kstamp;   // [2] in the control block (zeroed by k_pre)
+  uint32_t* kdone;    // [1] in the control block
   // per-workgroup scratch of the blob kernel
   uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
                       // (pathological blobs only; every other per-blob array lives in LDS)

@@ -141,6 +141,24 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 }
 
 
+// Device-clock span of one launch of the timed kernel (DevBufs::kt_stage): the
+// first workgroup (workgroups start in id order) stamps its start, every
+// workgroup counts itself done once its work is over (after a barrier) and the
+// last one stamps the end -- the kernel's execution span, as rocprofv3's kernel
+// trace times it, measured live without a profiler.  Off (no atomics) unless
+// this launch is the timed one.
+__device__ __forceinline__ void kt_begin(const DevBufs& b, int stage) {
+  if (b.kt_stage == stage && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 &&
+      threadIdx.y == 0)
+    b.kstamp[0] = wall_clock64();
+}
+__device__ __forceinline__ void kt_end(const DevBufs& b, int stage) {  // one thread per workgroup, work done
+  if (b.kt_stage != stage) return;
+  __threadfence();
+  const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
+  if (atomicAdd(b.kdone, 1u) == nb - 1) b.kstamp[1] = wall_clock64();
+}
+
 __constant__ float c_filter[7] = {0.01110899634659290314f, 0.13533528149127960205f, 0.60653066635131835938f,
                                   1.00000000000000000000f, 0.60653066635131835938f, 0.13533528149127960205f,
                                   0.01110899634659290314f};
@@ -296,6 +314,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint8_t s_rrun[kHC], s_crun[2][kHR];  // run starts along the halo row / columns
   __shared__ uint32_t s_nlr, s_nlk;
   if (tid == 0) { s_nlr = 0; s_nlk = 0; }
+  kt_begin(b, 1);
 
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
@@ -564,7 +583,10 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     if (cR && (wR & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
-  if (tid == 0) b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
+  if (tid == 0) {
+    b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
+    kt_end(b, 1);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -630,6 +652,7 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
 // a local root of the tile with a neighbour node (global union-find, atomicMin to
 // the smaller id, both finds in lockstep).
 __global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
+  kt_begin(b, 2);
   const int f = blockIdx.y;
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -639,6 +662,8 @@ __global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
     const uint2 e = list[k];
     g_union2(par, e.x, e.y);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) kt_end(b, 2);
 }
 
 // ---------------------------------------------------------------------------
@@ -788,6 +813,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
   const int f = blockIdx.z;
   const int tid = threadIdx.y * 64 + threadIdx.x;
+  kt_begin(b, 4);
   for (int i = tid; i < kLdsPairSlots; i += 256) {
     s_pkey[i] = 0;
     s_pcnt[i] = 0;
@@ -913,6 +939,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   if (tid == 0) {
     b.tcnt[tb] = min(total, (uint32_t)g.bnd_region);
     b.tent[tb] = s_nent;
+    kt_end(b, 4);
   }
 }
 
@@ -2890,6 +2917,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVES))) void k_extents(DevBufs b, Geom g) {
   __shared__ int64_t s_red[4][8];
+  kt_begin(b, 7);
   uint32_t cnt[kNumCls], total = 0, nlarge = 0;
 #pragma unroll
   for (int c = 0; c < kNumCls; c++) {
@@ -2902,13 +2930,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVE
     work_item(b, cnt, 0, kNumCls, it, &w);
     extents_item<256>(b, g, w, s_red);
   }
-  if (g.ctw == 32) return;  // latency mode: k_blob_small<true> does the small candidates itself
-  const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  for (uint32_t it = nlarge + gw; it < total; it += nw) {
-    uint32_t w = 0;
-    work_item(b, cnt, 0, kNumCls, it, &w);
-    extents_item<64>(b, g, w, nullptr);
+  if (g.ctw != 32) {  // latency mode: k_blob_small<true> does the small candidates itself
+    const uint32_t gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+    for (uint32_t it = nlarge + gw; it < total; it += nw) {
+      uint32_t w = 0;
+      work_item(b, cnt, 0, kNumCls, it, &w);
+      extents_item<64>(b, g, w, nullptr);
+    }
   }
+  __syncthreads();
+  if (threadIdx.x == 0) kt_end(b, 7);
 }
 
 // slowest item over the teams: probe[200 | 201] = (ticks << 20) | points; the
@@ -2939,6 +2970,7 @@ template <int NT, int CAP>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
+  kt_begin(b, 9);
   uint32_t* pacc = S.pacc;
   if (tid < 22) pacc[tid] = 0;
   if (tid == 0) S.slow_dt = 0;
@@ -2966,6 +2998,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   probe_flush_slow(b, prm, S, tid == 0);
   if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
   if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+  if (tid == 0) kt_end(b, 9);
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
@@ -2980,6 +3013,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
   const int wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   BlobShared<64, kSmallBlob>& S = Ss[wave];
+  kt_begin(b, 8);
   uint32_t* pacc = S.pacc;
   if (lane < 22) pacc[lane] = 0;
   if (lane == 0) S.slow_dt = 0;
@@ -3017,6 +3051,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
   probe_flush_slow(b, prm, S, lane == 0);
   if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
   if (lane == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+  if (b.kt_stage == 8) {  // (uniform: the timed launch only)
+    __syncthreads();
+    if (threadIdx.x == 0) kt_end(b, 8);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3091,6 +3129,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
   constexpr int RCAP = kMaxRefineSamples;
   __shared__ DecodeShared S;
   const int tid = threadIdx.x;
+  kt_begin(b, 10);
   double* gsx = b.rsamp + (size_t)blockIdx.x * (2 * (kMaxRefineSamples - kLdsRefine));
   double* gsy = gsx + (kMaxRefineSamples - kLdsRefine);
   // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
@@ -3488,6 +3527,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
   }
   }
   probe_flush(b, prm, pacc, 128, tid == 0);
+  if (tid == 0) kt_end(b, 10);
 }
 
 // ---------------------------------------------------------------------------

@@ -34,6 +34,7 @@ EXPORTS = [
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
     "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
     "at_draw_outlines_device", "at_detections", "at_max_detections", "at_annotate_staged", "at_enqueue_host",
+    "at_kernel_span",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39
@@ -177,6 +178,8 @@ def load_library(path: str = LIB_PATH):
     L.at_poses.argtypes = [C.c_void_p, C.c_int, C.POINTER(AtPose), C.c_int]
     L.at_set_kernel_timer.argtypes = [C.c_void_p, C.c_int]
     L.at_kernel_time.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
+    if hasattr(L, "at_kernel_span"):
+        L.at_kernel_span.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
     L.at_batch_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     L.at_tag_detections.argtypes = [C.POINTER(AtPose), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                     C.POINTER(AtTagDetection)]
@@ -425,9 +428,16 @@ class GpuDetector:
         _check(L.at_set_kernel_timer(self._h, stage), "at_set_kernel_timer")
 
     def kernel_time(self):
-        """(mean ms per launch, launches) of the timed kernel."""
+        """(mean ms per launch, launches) of the timed kernel (HIP events on its stream)."""
         ms, n = C.c_double(), C.c_longlong()
         _check(load_library().at_kernel_time(self._h, C.byref(ms), C.byref(n)), "at_kernel_time")
+        return ms.value, n.value
+
+    def kernel_span(self):
+        """(mean ms per launch, launches) of the timed kernel on the device clock (first
+        workgroup start -> last workgroup end; the span a rocprofv3 kernel trace times)."""
+        ms, n = C.c_double(), C.c_longlong()
+        _check(load_library().at_kernel_span(self._h, C.byref(ms), C.byref(n)), "at_kernel_span")
         return ms.value, n.value
 
     BATCH_STATS = ("frames", "boundary_points", "pairs", "small_blob_points", "large_blob_points",

@@ -360,6 +360,11 @@ def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     assert run(3) == base
     ms, launches = det.kernel_time()
     assert launches == 3 and ms > 0
+    span, nspan = det.kernel_span()  # device-clock span: every launch of a stamped kernel
+    if timed == "k_pose":
+        assert nspan == 0
+    else:
+        assert nspan == 3 and 0 < span <= ms * 1.05 + 0.005, (span, ms)
     det.set_kernel_timer(None)
     det.set_profiling(True)
     assert run() == base
