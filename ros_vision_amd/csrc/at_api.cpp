@@ -428,7 +428,9 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.det_head = sc + kCtlDetHead;
   b.kt_stage = -1;
   b.kstamp = reinterpret_cast<uint64_t*>(d->d_ctrl + d->kstamp_word);
-  b.kdone = d->d_ctrl + d->kstamp_word + 4;
+  b.kgrid = d->d_ctrl + d->kstamp_word + 4;
+  b.kwg_cap = (uint32_t)(B * 1024 + 4096);  // >= the workgroups of any stamped launch (1080p: 510 tiles per frame)
+  b.kwg = (uint64_t*)dalloc((size_t)b.kwg_cap * 2 * 8);
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)

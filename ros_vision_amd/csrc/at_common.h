@@ -259,8 +259,10 @@ struct DevBufs {
   // words of its first workgroup's start / last workgroup's end (wall clock) and
   // the count of finished workgroups that finds the last one
   int32_t kt_stage;
-  uint64_t* kstamp;   // [2] in the control block (zeroed by k_pre)
-  uint32_t* kdone;    // [1] in the control block
+  uint64_t* kstamp;   // [2] in the control block: span start / end (k_kt_span)
+  uint32_t* kgrid;    // [1] in the control block: workgroups of the timed launch
+  uint64_t* kwg;      // [2][kwg_cap] each workgroup's start / end stamp (plain stores)
+  uint32_t kwg_cap;
   // per-workgroup scratch of the blob kernel
   uint64_t* s_pk;     // [nblobwg][kSortCap/2] peak keys beyond a large-blob team's LDS peak area
                       // (pathological blobs only; every other per-blob array lives in LDS)

@@ -141,22 +141,46 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 }
 
 
-// Device-clock span of one launch of the timed kernel (DevBufs::kt_stage): the
-// first workgroup (workgroups start in id order) stamps its start, every
-// workgroup counts itself done once its work is over (after a barrier) and the
-// last one stamps the end -- the kernel's execution span, as rocprofv3's kernel
-// trace times it, measured live without a profiler.  Off (no atomics) unless
-// this launch is the timed one.
+// Device-clock span of one launch of the timed kernel (DevBufs::kt_stage): every
+// workgroup stores its start and, once its work is over, its end on the GPU wall
+// clock (plain stores into its own slots: no shared counter to contend on);
+// k_kt_span, launched after the timed kernel, reduces them to the first start
+// and the last end -- the kernel's execution span, as rocprofv3's kernel trace
+// times it, measured live without a profiler.  Nothing is stored unless this
+// launch is the timed one.
+__device__ __forceinline__ uint32_t kt_wg_id() {
+  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
 __device__ __forceinline__ void kt_begin(const DevBufs& b, int stage) {
-  if (b.kt_stage == stage && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 &&
-      threadIdx.y == 0)
-    b.kstamp[0] = wall_clock64();
+  if (b.kt_stage != stage || threadIdx.x != 0 || threadIdx.y != 0) return;
+  const uint32_t id = kt_wg_id();
+  if (id == 0) *b.kgrid = gridDim.x * gridDim.y * gridDim.z;
+  if (id < b.kwg_cap) b.kwg[id] = wall_clock64();
 }
 __device__ __forceinline__ void kt_end(const DevBufs& b, int stage) {  // one thread per workgroup, work done
   if (b.kt_stage != stage) return;
-  __threadfence();
-  const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
-  if (atomicAdd(b.kdone, 1u) == nb - 1) b.kstamp[1] = wall_clock64();
+  const uint32_t id = kt_wg_id();
+  if (id < b.kwg_cap) b.kwg[b.kwg_cap + id] = wall_clock64();
+}
+__global__ __launch_bounds__(256) void k_kt_span(DevBufs b) {
+  __shared__ uint64_t s_mn[4], s_mx[4];
+  const uint32_t n = min(*b.kgrid, b.kwg_cap);
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    mn = min(mn, b.kwg[i]);
+    mx = max(mx, b.kwg[b.kwg_cap + i]);
+  }
+  mn = wave_reduce(mn, MinOp());
+  mx = wave_reduce(mx, MaxOp());
+  if (lane_id() == 0) { s_mn[threadIdx.x >> 6] = mn; s_mx[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0 && n) {
+    for (int w = 1; w < 4; w++) { mn = min(mn, s_mn[w]); mx = max(mx, s_mx[w]); }
+    mn = min(mn, s_mn[0]);
+    mx = max(mx, s_mx[0]);
+    b.kstamp[0] = mn;
+    b.kstamp[1] = mx;
+  }
 }
 
 __constant__ float c_filter[7] = {0.01110899634659290314f, 0.13533528149127960205f, 0.60653066635131835938f,
@@ -3909,6 +3933,10 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   }
   tk(10, st, 1);
   mark();
+  // the timed kernel's device-clock span (after it, outside its timing events;
+  // before k_pose hands the control block to the host)
+  if (b.kt_stage >= 1 && b.kt_stage <= 10 && b.kt_stage != 3 && b.kt_stage != 5 && b.kt_stage != 6)
+    hipLaunchKernelGGL(k_kt_span, dim3(1), dim3(256), 0, st, b);
   tk(11, st, 0);
   // latency mode: a wave per detection; throughput mode: four lanes per detection
   if (prm.tag_size > 0 && on(11)) {

@@ -14,10 +14,13 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-SHORT="$ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 4 --warmup 1 --latency-frames 0"
+# every profiled run is the timed loop alone (no host-ingest / C3 / latency legs), so
+# the per-frame PMC figures and the rocprof averages describe the bench's timed launches
+ONLY="--latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0"
+SHORT="$ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 4 --warmup 1 $ONLY"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
-  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --timed-kernel ${TIMED:-k_blob_small} --batch $BATCH --steps 40 --warmup 3 --latency-frames 0 \
+  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --timed-kernel ${TIMED:-k_blob_small} --batch $BATCH --steps 40 --warmup 3 $ONLY \
   > "$OUT/trace_timed_bench.json" 2> "$OUT/trace_timed.err"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $SHORT \
   > /dev/null 2> "$OUT/pmc_fetch.err"
@@ -38,5 +41,6 @@ cd "$ROOT"
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" "$OUT/pmc_write/run_counter_collection.csv" $BATCH 1280 720 "$OUT/pmc_traffic.json" > /dev/null
 cp "$OUT/pmc_traffic.json" profiles/pmc_traffic.json  # the bench line below reads it
 python3 tools/pmc_agg.py "$OUT/pmc_sq_a/run_counter_collection.csv" "$OUT/pmc_sq_b/run_counter_collection.csv" > "$OUT/sq_counters_agg.txt"
+python3 tools/timed_launches.py "$OUT/trace_timed/run_kernel_trace.csv" "$OUT/trace_timed_bench.json" > "$OUT/timed_launches.json"
 timeout -k 10 400 python3 bench.py --batch $BATCH > "$OUT/bench.json" 2> "$OUT/bench.err"
 find "$OUT" -name "*.csv" | sort
