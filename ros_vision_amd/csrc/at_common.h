@@ -25,11 +25,6 @@ struct CclTile {
 };
 constexpr int kCclTileH = 32;
 constexpr int kCclTileNodesMax = CclTile<64>::NODES;  // stride of the per-tile local-root lists
-// cross-tile links of one CCL tile (k_thr_ccl -> k_ccl_border): at most 5 per top-row
-// block, 3 per left-column block, 1 per right-column block
-constexpr int kBorderLinkCap = 5 * CclTile<64>::BW + 3 * CclTile<64>::BH + CclTile<64>::BH;
-constexpr int kLinkHashBits = 9;
-constexpr int kLinkHash = 1 << kLinkHashBits;  // LDS dedup table of a tile's links (>= 2 x kBorderLinkCap)
 // per-frame open-addressing table of blob pairs: 4096 slots hold every frame the
 // 12-bit blob index admits (<= kMaxPairs keys; typical frames fill ~10 %), and keep
 // k_pairs' LDS copy at 84 KB so it co-resides with other kernels' workgroups
@@ -201,8 +196,6 @@ struct DevBufs {
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
   uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodesMax] local roots of each CCL tile (global node ids)
   uint32_t* nlroot;   // [B][CTX*CTY]
-  uint2* blink;       // [B][CTX*CTY][kBorderLinkCap] cross-tile links (local root, neighbour node)
-  uint32_t* nblink;   // [B][CTX*CTY]
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile

@@ -334,10 +334,8 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint8_t s_t[kHR][kHC + 2];  // thr of rows y0-1..y0+H-1, cols x0-1..x0+W (+pad)
   __shared__ uint32_t s_par[kCclTileNodes];
   __shared__ uint32_t s_cnt[kCclTileNodes];
-  __shared__ uint32_t s_lk[kLinkHash];  // dedup table of the tile's cross-tile links
-  __shared__ uint8_t s_rrun[kHC], s_crun[2][kHR];  // run starts along the halo row / columns
-  __shared__ uint32_t s_nlr, s_nlk;
-  if (tid == 0) { s_nlr = 0; s_nlk = 0; }
+  __shared__ uint32_t s_nlr;
+  if (tid == 0) s_nlr = 0;
   kt_begin(b, 1);
 
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
@@ -402,31 +400,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     }
   }
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
-  for (int i = tid; i < kLinkHash; i += NT) s_lk[i] = 0;
   __syncthreads();
-  // run starts (prefix max of the run breaks, one wave scan each) of the halo row
-  // (wave 0) and the left / right halo columns (waves 1, 2): the cross-tile links
-  // into one run are one union (below)
-  {
-    const int w = tid >> 6, l = tid & 63;
-    if (w == 0) {
-      const uint32_t brk = (l < kHC && (l == 0 || s_t[0][l - 1] != s_t[0][l])) ? (uint32_t)l : 0u;
-      const uint32_t st = wave_incl_scan(brk, MaxOp(), 0u);
-      if (l < kHC) s_rrun[l] = (uint8_t)st;
-      if (l == 63) {
-        uint32_t r = st;
-        for (int cc = 64; cc < kHC; cc++) {
-          if (s_t[0][cc - 1] != s_t[0][cc]) r = (uint32_t)cc;
-          s_rrun[cc] = (uint8_t)r;
-        }
-      }
-    } else if (w <= 2) {
-      const int col = w == 1 ? 0 : kHC - 1;
-      const uint32_t brk = (l < kHR && (l == 0 || s_t[l - 1][col] != s_t[l][col])) ? (uint32_t)l : 0u;
-      const uint32_t st = wave_incl_scan(brk, MaxOp(), 0u);
-      if (l < kHR) s_crun[w - 1][l] = (uint8_t)st;
-    }
-  }
   // write this tile's threshold plane (4 bytes per thread)
   {
     const int r = tid / (kCclTileW / 4), c4 = (tid % (kCclTileW / 4)) * 4;
@@ -513,69 +487,17 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     if (nbl) atomicOr(&s_cnt[rL], kTouchBit);
     if (nbr) atomicOr(&s_cnt[rR], kTouchBit);
   }
-  auto gid = [&](uint32_t s) -> uint32_t {  // global node id of a tile node slot
-    const int sty = s / kCclRowNodes, r = s % kCclRowNodes;
-    const int gy = y0 / 2 + sty;
-    if (r < kCclBW) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
-    const int k = r - kCclBW;
-    return (uint32_t)((2 * gy + 1) * g.Wd + 2 * (x0 / 2 + (k >> 1)) + (k & 1));
-  };
-  const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
-  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
-  // Cross-tile unions (the reference's Merge over the tile borders,
-  // labeling_allegretti_2019_BKE.cu:302-338): this tile's top block row links up
-  // (P, Q, R, background Q for both columns), its left column left (S, background S,
-  // and P below the top row), its right column up-right (R below the top row) -- all
-  // decided here from the threshold halo.  A link joins this tile's node (by its
-  // local root, final now) to a neighbour node; neighbour pixels in one run of the
-  // halo row or column (consecutive pixels of one value) are connected, so links
-  // from one local root into one run are one union: the list k_ccl_border merges
-  // holds one entry per (local root, run).
-  if (BY < g.BH && BX < g.BW && (bty == 0 || btx == 0 || btx == kCclBW - 1)) {
-    const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX), idL = idF + g.Wd, idR = idL + 1;
-    const uint32_t Wd2 = 2u * (uint32_t)g.Wd;
-    uint2* out = b.blink + tl * kBorderLinkCap;
-    auto row_run = [&](int cc) { return (int)s_rrun[cc]; };  // run start in the halo row (s_t row 0)
-    auto col_run = [&](int col, int r) { return (int)s_crun[col == 0 ? 0 : 1][r]; };  // ... in a halo column
-    auto add = [&](uint32_t uslot, int region, int start, uint32_t v) {
-      const uint32_t key = ((uslot + 1) << 10) | ((uint32_t)region << 8) | (uint32_t)start;
-      uint32_t h = (key * 2654435761u) >> (32 - kLinkHashBits);
-      while (true) {
-        const uint32_t prev = atomicCAS(&s_lk[h], 0u, key);
-        if (prev == key) return;  // the same local root into the same run: already a union
-        if (prev == 0) {
-          const uint32_t o = atomicAdd(&s_nlk, 1u);
-          out[o] = make_uint2(gid(uslot), v);
-          return;
-        }
-        h = (h + 1) & (kLinkHash - 1);
-      }
-    };
-#define T(rr, cc) s_t[(rr) + 1][(cc) + 1]
-    const int pr = 2 * bty, pc = 2 * btx;
-    if (bty == 0 && y0 > 0) {  // up into the tile row above: halo row y0 - 1
-      if (a == 255 && T(-1, pc - 1) == 255) add(rF, 0, row_run(pc), idF - Wd2 - 2);
-      if ((a == 255 || bb == 255) && (T(-1, pc) == 255 || T(-1, pc + 1) == 255))
-        add(rF, 0, row_run(T(-1, pc) == 255 ? pc + 1 : pc + 2), idF - Wd2);
-      if (bb == 255 && T(-1, pc + 2) == 255) add(rF, 0, row_run(pc + 3), idF - Wd2 + 2);
-      if (a == 0 && T(-1, pc) == 0) add(rL, 0, row_run(pc + 1), idL - Wd2);
-      if (bb == 0 && T(-1, pc + 1) == 0) add(rR, 0, row_run(pc + 2), idR - Wd2);
-    }
-    if (btx == 0 && x0 > 0) {  // left into the tile to the left: halo column x0 - 1
-      if (bty > 0 && a == 255 && T(pr - 1, -1) == 255) add(rF, 1, col_run(0, pr), idF - Wd2 - 2);
-      if ((a == 255 || c == 255) && (T(pr, -1) == 255 || T(pr + 1, -1) == 255))
-        add(rF, 1, col_run(0, T(pr, -1) == 255 ? pr + 1 : pr + 2), idF - 2);
-      if ((a == 0 && T(pr, -1) == 0) || (c == 0 && T(pr + 1, -1) == 0))
-        add(rL, 1, col_run(0, (a == 0 && T(pr, -1) == 0) ? pr + 1 : pr + 2), idL - 1);
-    }
-    if (btx == kCclBW - 1 && bty > 0 && bb == 255 && T(pr - 1, pc + 2) == 255)  // up-right: halo column x0 + W
-      add(rF, 2, col_run(kHC - 1, pr), idF - Wd2 + 2);
-#undef T
-  }
   __syncthreads();
-  if (tid == 0) b.nblink[tl] = s_nlk;
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
+  const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
   if (BY < g.BH && BX < g.BW) {
+    auto gid = [&](uint32_t s) -> uint32_t {
+      const int sty = s / kCclRowNodes, r = s % kCclRowNodes;
+      const int gy = y0 / 2 + sty;
+      if (r < kCclBW) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
+      const int k = r - kCclBW;
+      return (uint32_t)((2 * gy + 1) * g.Wd + 2 * (x0 / 2 + (k >> 1)) + (k & 1));
+    };
     uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
     uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
     const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
@@ -601,6 +523,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     }
     // the tile's local roots of components reaching its border (with pixels), for
     // k_ccl_roots / k_ccl_keep
+    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
     uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
     if (cF && (wF & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
     if (cL && (wL & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
@@ -672,22 +595,72 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
   }
 }
 
-// The cross-tile unions k_thr_ccl listed, one wave per CCL tile: every entry joins
-// a local root of the tile with a neighbour node (global union-find, atomicMin to
-// the smaller id, both finds in lockstep).
-__global__ __launch_bounds__(64) void k_ccl_border(DevBufs b, Geom g) {
+// One candidate union per thread (the reference's Merge, labeling_allegretti_2019_BKE.cu:302-338,
+// over the tile's border blocks): threads 0..5*BW-1 the top block row (BW blocks x
+// P, Q, R and the two background links), then the left block column (BH x P, S,
+// background S), then the right column (BH-1 x R).  Every union is one short
+// chain of global round trips instead of up to five in a row per lane.
+template <int TW>
+struct BorderRoles {
+  static constexpr int Top = 5 * CclTile<TW>::BW, Left = 3 * CclTile<TW>::BH, Right = CclTile<TW>::BH - 1;
+  static constexpr int NT = (Top + Left + Right + 63) / 64 * 64;
+};
+template <int TWD>
+__global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, Geom g) {
+  constexpr int kBorderTop = BorderRoles<TWD>::Top, kBorderLeft = BorderRoles<TWD>::Left,
+                kBorderRight = BorderRoles<TWD>::Right;
+  constexpr int kCclBW = CclTile<TWD>::BW, kCclBH = CclTile<TWD>::BH;
   kt_begin(b, 2);
-  const int f = blockIdx.y;
-  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
-  uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
-  const uint32_t n = b.nblink[tl];
-  const uint2* list = b.blink + tl * kBorderLinkCap;
-  for (uint32_t k = threadIdx.x; k < n; k += 64) {
-    const uint2 e = list[k];
-    g_union2(par, e.x, e.y);
+  const int f = blockIdx.z;
+  const int t = threadIdx.x;
+  int bty = 0, btx = 0, role = 3, kind = 0;  // role 3: no candidate (padding threads)
+  if (t < kBorderTop) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
+  else if (t < kBorderTop + kBorderLeft) { role = 1; bty = (t - kBorderTop) / 3; btx = 0; kind = (t - kBorderTop) % 3; }
+  else if (t < kBorderTop + kBorderLeft + kBorderRight) {
+    role = 2; bty = t - (kBorderTop + kBorderLeft) + 1; btx = kCclBW - 1; kind = 0;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) kt_end(b, 2);
+  const int BY = blockIdx.y * kCclBH + bty, BX = blockIdx.x * kCclBW + btx;
+  if (BY >= g.BH || BX >= g.BW) role = 3;
+  const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
+  uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
+  const int Wd = g.Wd;
+  const int row = 2 * BY, col = 2 * BX;
+  const size_t idx = (size_t)row * Wd + col;
+  auto px = [&](int r, int c) -> uint8_t {
+    if (r < 0 || c < 0 || r >= g.Hd || c >= g.Wd) return 127;
+    return thr[(size_t)r * Wd + c];
+  };
+  const bool act = role != 3;  // (no loads outside the image for the padding threads)
+  const uint8_t a = act ? thr[idx] : 127, bb = act ? thr[idx + 1] : 127, c = act ? thr[idx + Wd] : 127;
+  const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
+  uint32_t u = 0, v = 0;
+  bool link = false;
+  if (role == 0 && BY > 0) {
+    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255);
+      u = F; v = F - 2 * Wd;
+    }
+    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2; }
+    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - 2 * Wd; }
+    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - 2 * Wd; }
+  } else if (role == 1 && BX > 0) {
+    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255);
+      u = F; v = F - 2;
+    } else {
+      link = (a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0);
+      u = L; v = L - 1;
+    }
+  } else if (role == 2 && BY > 0) {
+    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
+  }
+  if (link) g_union2(par, u, v);
+  if (b.kt_stage == 2) {  // (uniform: the timed launch only)
+    __syncthreads();
+    if (t == 0) kt_end(b, 2);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3854,7 +3827,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(1, st, 1);
     mark();
     tk(2, st, 0);
-    if (on(2)) hipLaunchKernelGGL(k_ccl_border, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
+    if (!on(2)) {}
+    else if (g.ctw == 32) hipLaunchKernelGGL(k_ccl_border<32>, grd, dim3(BorderRoles<32>::NT), 0, st, b, g);
+    else hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
     tk(2, st, 1);
     mark();
   }
