@@ -11,7 +11,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in $ORDER; do
     echo -n "round=$r lib=$lib " >> $OUT/r.txt
     AT_HIP_LIB=$lib timeout -k 10 150 python3 bench.py --instances $inst --batch $batch --hw-queues $hwq --pool 128 \
-      --steps ${STEPS:-100} --warmup 5 --no-cpu-baseline --latency-frames ${LATFRAMES:-0} --no-stage-profile --no-kernel-timer \
+      --steps ${STEPS:-100} --warmup 5 --no-cpu-baseline --latency-frames ${LATFRAMES:-0} --host-ingest-steps 0 --c3-latency-iters 0 --no-stage-profile --no-kernel-timer \
       2>>$OUT/err.txt | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['value'], j['ms_per_step'], j['p50_latency_hbm_ms'])" >> $OUT/r.txt || exit 1
   done
 done
