@@ -2067,22 +2067,26 @@ __device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, in
 // fit twice in S.keys (n > KEYS / 2): the keys stay in registers (CAP / NT per
 // thread) through the counting sort and the in-bucket rank, instead of falling
 // back to a bitonic sort of the next power of two.
+// keys in registers (slot t = j * NT + tid); on failure they are left in S.keys
+// (load order) for the bitonic fallback
 template <int NT, int CAP>
-__device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp, int n) {
+__device__ bool team_reg_bucket_sort_kv(BlobShared<NT, CAP>& S, uint64_t (&kv)[CAP / NT], int n) {
   static_assert(NT > 64 && CAP % NT == 0, "workgroup teams");
   constexpr int KPL = CAP / NT;
   constexpr int KEYS = kKeySlots<NT, CAP>;
   static_assert(KPL <= 16, "at most 16 keys per thread");
   const int tid = team_rank<NT>();
-  uint64_t kv[KPL];
-#pragma unroll
-  for (int j = 0; j < KPL; j++) {
-    const int t = j * NT + tid;
-    kv[j] = t < n ? grp[t] : ~0ull;
-  }
   int nb = 32;
   while (2 * nb < n) nb <<= 1;  // n/2 <= nb < n, power of two
-  if (nb / 2 > KEYS / 4) return false;
+  if (nb / 2 > KEYS / 4) {  // (uniform)
+#pragma unroll
+    for (int j = 0; j < KPL; j++) {
+      const int t = j * NT + tid;
+      if (t < n) S.keys[t] = kv[j];
+    }
+    team_sync<NT>();
+    return false;
+  }
   const int sh = 26 - __builtin_ctz((unsigned)nb);
   auto bucket = [&](uint64_t k) { return (uint32_t)((k >> kKeyTheta) >> sh); };
   uint32_t* bcnt = S.bcnt;
@@ -2166,6 +2170,19 @@ __device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp
     if (j * NT + tid < n) S.keys[rk[j]] = kv[j];
   team_sync<NT>();
   return true;
+}
+
+template <int NT, int CAP>
+__device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp, int n) {
+  constexpr int KPL = CAP / NT;
+  const int tid = team_rank<NT>();
+  uint64_t kv[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; j++) {
+    const int t = j * NT + tid;
+    kv[j] = t < n ? grp[t] : ~0ull;
+  }
+  return team_reg_bucket_sort_kv<NT, CAP>(S, kv, n);
 }
 
 // Inclusive prefix moments P(i) of the blob's points: the owning chunk's base
@@ -2272,6 +2289,88 @@ __device__ bool small_extents_keys(const DevBufs& b, const Geom& g, int f, uint3
   return true;
 }
 
+// Latency mode, large candidates (> kSmallBlob points, a workgroup team): the
+// same as small_extents_keys -- MinMaxExtents, SelectBlobs, the (theta, plane, y,
+// x) keys with the line-fit weight in registers (slot t = j * NT + tid) -- so
+// k_extents drops out of the B = 1 chain.  Returns SelectBlobs' decision
+// (uniform across the team).
+template <int NT, int CAP>
+__device__ bool large_extents_keys(const DevBufs& b, const Geom& g, BlobShared<NT, CAP>& S, int f, uint32_t rank,
+                                   uint32_t n, const uint64_t* grp, uint64_t (&kv)[CAP / NT]) {
+  constexpr int U = CAP / NT;
+  const int tid = team_rank<NT>();
+  const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t t = (uint32_t)(u * NT + tid);
+    kv[u] = t < n ? grp[t] : 0;
+  }
+  uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
+  int32_t sgx = 0, sgy = 0;
+  int64_t spg = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if ((uint32_t)(u * NT + tid) >= n) continue;
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const uint32_t px = ((k >> 14) & 0x3ff) * 2 + dx_of(dxy);
+    const uint32_t py = ((k >> 4) & 0x3ff) * 2 + dy_of(dxy);
+    const bool b2w = (k & 8) != 0;
+    const int gx = b2w ? dx_of(dxy) : -dx_of(dxy), gy = b2w ? dy_of(dxy) : -dy_of(dxy);
+    mnx = min(mnx, px); mxx = max(mxx, px); mny = min(mny, py); mxy = max(mxy, py);
+    sgx += gx; sgy += gy;
+    spg += (int64_t)px * gx + (int64_t)py * gy;
+  }
+  team_extents<NT, CAP>(S, mnx, mxx, mny, mxy, sgx, sgy, spg);
+  Ext e;
+  e.min_x = mnx; e.max_x = mxx; e.min_y = mny; e.max_y = mxy;
+  e.gx_sum = sgx; e.gy_sum = sgy; e.pg_sum = spg;
+  e.count = n;
+  bool keep = (int)((e.max_x - e.min_x) * (e.max_y - e.min_y)) >= g.min_tag_width;
+  keep = keep && !((double)ext_dot(e) < 0.0);
+  if (!keep) return false;
+  if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;  // (parity taps, host statistics)
+  const double cx = ext_cx(e), cy = ext_cy(e);
+  uint32_t gp[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const int32_t ix = (int32_t)(((k >> 14) & 0x3ff) * 2 + dx_of(dxy) + 1) / 2;
+    const int32_t iy = (int32_t)(((k >> 4) & 0x3ff) * 2 + dy_of(dxy) + 1) / 2;
+    const bool in = (uint32_t)(u * NT + tid) < n && ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd;
+    const int32_t at = in ? iy * g.Wd + ix : g.Wd + 1;
+    gp[u] = (uint32_t)dec[at - 1] | ((uint32_t)dec[at + 1] << 8) | ((uint32_t)dec[at - g.Wd] << 16) |
+            ((uint32_t)dec[at + g.Wd] << 24);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if ((uint32_t)(u * NT + tid) >= n) {
+      kv[u] = ~0ull;
+      continue;
+    }
+    const uint64_t k = kv[u];
+    const int dxy = (int)(k & 3);
+    const uint32_t bx = (k >> 14) & 0x3ff, by = (k >> 4) & 0x3ff;
+    const uint32_t px = bx * 2 + dx_of(dxy), py = by * 2 + dy_of(dxy);
+    const float dyf = (float)((double)py - cy);
+    const float dxf = (float)((double)px - cx);
+    const float theta = (float)(((double)det_atan2f(dyf, dxf) + 3.14159265358979323846) * 8e6);
+    long long ti = (long long)rintf(theta);
+    if (ti < 0) ti = 0;
+    const int32_t ix = (int32_t)(px + 1) / 2, iy = (int32_t)(py + 1) / 2;
+    int32_t Wt = 1;
+    if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
+      const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
+      const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
+      Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+    }
+    kv[u] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
+            ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
+  }
+  return true;
+}
+
 // Processes one work item (frame, pair rank) with a team of NT threads.
 // gpk: this team's global overflow area for peak keys beyond kPeakCap (large
 // blobs only; nullptr when the LDS area always suffices).
@@ -2320,7 +2419,15 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   // extents, SelectBlobs and the theta keys: from k_extents, or here (FUSE)
   bool sorted = false, in_lds = false;
   const uint32_t bi = rank & 0xfff;
-  if constexpr (NT == 64 && FUSE) {
+  if constexpr (NT > 64 && FUSE) {
+    uint64_t kv[CAP / NT];
+    if (!large_extents_keys<NT, CAP>(b, g, S, f, rank, n, grp, kv)) return;  // uniform across the team
+    if (tid == 0) pacc[20] += n;
+    phase(0);
+    phase(1);
+    sorted = team_reg_bucket_sort_kv<NT, CAP>(S, kv, (int)n);  // n > kSmallBlob >= 64
+    in_lds = true;
+  } else if constexpr (NT == 64 && FUSE) {
     uint64_t kv[kSmallBlob / 64];
     if (!small_extents_keys(b, g, f, rank, n, grp, kv)) return;  // uniform across the wave
     if (tid == 0) pacc[20] += n;
@@ -2963,7 +3070,7 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
 
 // K9a (large blobs, > kSmallBlob points): one blob per NT-thread workgroup
 // iteration, persistent over the large work list.
-template <int NT, int CAP>
+template <int NT, int CAP, bool FUSE = false>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
@@ -2988,7 +3095,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
     if (item >= nwork) break;
     uint32_t w = 0;
     work_item(b, s_cnt, 0, kNumLargeCls, item, &w);
-    blob_item<NT, CAP>(b, g, prm, S, gpk, s_combo, w, load_pair_info(b, w), pacc);
+    blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w), pacc);
   }
   __syncthreads();
   probe_flush(b, prm, pacc, 80, tid == 0);
@@ -3858,7 +3965,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   tk(6, st, 1);
   mark();
   tk(7, st, 0);
-  if (on(7)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
+  // (latency mode: the blob kernels do k_extents' work themselves, up to 4096-point blobs)
+  if (on(7) && (g.ctw != 32 || g.max_cluster > 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
   tk(7, st, 1);
   mark();
   auto blob_large = [&](hipStream_t s) {
@@ -3866,7 +3974,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     // LDS sized for the largest blob the geometry admits (max_cluster = 2 (W + H))
     const bool cap4k = g.max_cluster <= 4096;
     if (!on(9)) return;
-    if (B < kWideBlobMaxBatch || prm.wide_blob) {
+    if (g.ctw == 32 && cap4k) {  // latency mode: extents, SelectBlobs and keys in the blob team (no k_extents)
+      hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+    } else if (B < kWideBlobMaxBatch || prm.wide_blob) {
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
     } else {
