@@ -341,19 +341,15 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   // the tile's decimated pixels (+1 halo) are loaded together with the tile
-  // min/max: one global round trip instead of two.  Aligned dwords covering
-  // columns x0-4 .. x0+W+3 (Wd % 4 == 0: a dword is wholly in or out of the
-  // image) into LDS, two per thread instead of five byte loads
-  constexpr int kDW = (kCclTileW + 8) / 4;  // dwords per halo row
-  constexpr int kDecDw = kHR * kDW;
-  __shared__ uint32_t s_dec[kHR][kDW];
-  for (int j = tid; j < kDecDw; j += NT) {
-    const int r = j / kDW, c = j % kDW;
-    const int y = y0 - 1 + r, x = x0 - 4 + 4 * c;
-    s_dec[r][c] = (y >= 0 && y < g.Hd && x >= 0 && x < g.Wd)
-                      ? *reinterpret_cast<const uint32_t*>(dec + (size_t)y * g.Wd + x) : 0u;
-  }
+  // min/max: one global round trip instead of two
   constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
+  uint8_t dv[kDecPer];
+#pragma unroll
+  for (int k = 0; k < kDecPer; k++) {
+    const int i = tid + NT * k;
+    const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
+    dv[k] = (i < kHR * kHC && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? dec[(size_t)y * g.Wd + x] : 0;
+  }
   for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
     const int r = i / (kTW + 4), c = i % (kTW + 4);
     const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
@@ -397,8 +393,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
           res = 127;
         } else {
           const uint8_t th = (uint8_t)(mn + (mx - mn) / 2);
-          const uint8_t dv = reinterpret_cast<const uint8_t*>(&s_dec[r][0])[c + 3];  // column x0 - 1 + c
-          res = dv > th ? 255 : 0;
+          res = dv[k] > th ? 255 : 0;
         }
       }
       s_t[r][c] = res;
