@@ -828,92 +828,38 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   constexpr int kPer = (kTN + 255) / 256;
   // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
   // column) -> local root -> component root | kept bit (k_ccl_roots, k_ccl_keep;
-  // a local root's own word already holds root | kept, so the second hop masks).
-  // Staged per 2x2 block, not per pixel: the tile's 9 x 33 blocks' three nodes
-  // (F, L, R) take both hops (891 + 891 loads instead of 2244 + 1122), the
-  // threshold rows come as dwords; every pixel then picks its node's label from
-  // LDS.  The block labels live in the point stage's storage until the points
-  // start (after the barrier below).
-  constexpr int kBR = kTR / 2 + 1, kBC = kTC / 2;  // 9 block rows, 33 block columns
-  constexpr int kNB = kBR * kBC;
-  static_assert(3 * kNB * 4 <= (int)sizeof(s_pts), "block labels fit the point stage");
-  uint32_t* s_blab = reinterpret_cast<uint32_t*>(s_pts);  // [3][kNB]: F, L, R label | kept bit
-  const int by0 = (ty0 - 1) / 2, bx0 = tx0 / 2;          // first block row / column of the tile
-  constexpr int kBPer = (kNB + 255) / 256;
-  uint32_t bp[kBPer][3];
+  // a local root's own word already holds root | kept, so the second hop masks)
+  // (the threshold byte and both candidate nodes' parents are loaded together,
+  // the byte then picks fg or bg: one round trip fewer than thr -> node -> parent)
+  uint32_t lv[kPer], lb[kPer];
+  uint8_t tv[kPer];
 #pragma unroll
-  for (int k = 0; k < kBPer; k++) {
-    const int j = tid + 256 * k;
-    const int BY = by0 + j / kBC, BX = bx0 + j % kBC;
-    bp[k][0] = bp[k][1] = bp[k][2] = 0xffffffffu;
-    if (j < kNB && 2 * BY < g.Hd && 2 * BX < Wd) {
-      const uint32_t F = (uint32_t)(2 * BY * Wd + 2 * BX);
-      bp[k][0] = par[F];
-      bp[k][1] = par[F + Wd];
-      bp[k][2] = par[F + Wd + 1];
-    }
-  }
-  // threshold rows ty0.. of the tile (cols x0-1..x0+64; Wd % 4 == 0, tx0 % 64 == 0:
-  // dword-aligned), raw into s_tthr; out of the image -> 127
-  constexpr int kDW = (kTC + 3) / 4;  // 17 dwords per row
-  constexpr int kTPer = (kTR * kDW + 255) / 256;
-  uint32_t tw[kTPer];
-#pragma unroll
-  for (int k = 0; k < kTPer; k++) {
-    const int j = tid + 256 * k;
-    const int yy = ty0 + j / kDW, xx = tx0 + 4 * (j % kDW);
-    tw[k] = 0x7f7f7f7fu;
-    if (j < kTR * kDW && yy < g.Hd) {
-      const uint8_t* row = thr + (size_t)yy * Wd;
-      if (xx + 3 < Wd) {
-        tw[k] = *reinterpret_cast<const uint32_t*>(row + xx);
-      } else {
-        for (int q = 0; q < 4; q++)
-          if (xx + q < Wd) tw[k] = (tw[k] & ~(0xffu << (8 * q))) | ((uint32_t)row[xx + q] << (8 * q));
-      }
+  for (int k = 0; k < kPer; k++) {
+    const int e = tid + 256 * k;
+    const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
+    lv[k] = 0xffffffffu;
+    lb[k] = 0xffffffffu;
+    tv[k] = 127;
+    if (e < kTN && yy < g.Hd && xx < Wd) {
+      const size_t i = (size_t)yy * Wd + xx;
+      tv[k] = thr[i];
+      const uint32_t F = (uint32_t)((yy & ~1) * Wd + (xx & ~1));
+      lv[k] = par[F];
+      lb[k] = par[F + Wd + (xx & 1)];
     }
   }
 #pragma unroll
-  for (int k = 0; k < kBPer; k++)
-#pragma unroll
-    for (int n = 0; n < 3; n++)
-      if (bp[k][n] != 0xffffffffu) bp[k][n] = par[bp[k][n] & ~kKeptBit];
-#pragma unroll
-  for (int k = 0; k < kBPer; k++) {
-    const int j = tid + 256 * k;
-    if (j < kNB) {
-#pragma unroll
-      for (int n = 0; n < 3; n++) {
-        uint32_t v = bp[k][n];
-        if constexpr (!KEPT) {  // latency mode: the size plane at the component root
-          if (v != 0xffffffffu) v = (v & ~kKeptBit) | (b.size[fo + (v & ~kKeptBit)] >= 25 ? kKeptBit : 0u);
-        }
-        s_blab[n * kNB + j] = v;
-      }
-    }
+  for (int k = 0; k < kPer; k++) {
+    lv[k] = tv[k] == 127 ? 0xffffffffu : (tv[k] == 255 ? lv[k] : lb[k]);
+    if (lv[k] != 0xffffffffu) lv[k] = par[lv[k] & ~kKeptBit];
   }
-#pragma unroll
-  for (int k = 0; k < kTPer; k++) {
-    const int j = tid + 256 * k;
-    if (j < kTR * kDW) {
-      const int r = j / kDW, c = 4 * (j % kDW);
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (c + q < kTC) s_tthr[r * kTC + c + q] = (uint8_t)(tw[k] >> (8 * q));
-    }
-  }
-  __syncthreads();  // block labels and raw threshold bytes in LDS
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     if (e < kTN) {
-      const int ly = e / kTC, lx = e % kTC;
-      const uint8_t tv = s_tthr[e];
-      const int j = ((ty0 + ly) / 2 - by0) * kBC + (tx0 + lx) / 2 - bx0;
-      const uint32_t lv = tv == 255 ? s_blab[j] : (tv == 0 ? s_blab[(1 + ((tx0 + lx) & 1)) * kNB + j] : 0xffffffffu);
-      const bool kept = lv != 0xffffffffu && (lv & kKeptBit) != 0;
-      s_tlab[e] = lv & ~kKeptBit;
-      s_tthr[e] = kept ? tv : (uint8_t)127;
+      const bool kept = lv[k] != 0xffffffffu && (KEPT ? (lv[k] & kKeptBit) != 0 : b.size[fo + lv[k]] >= 25);
+      s_tlab[e] = lv[k] & ~kKeptBit;
+      s_tthr[e] = kept ? tv[k] : (uint8_t)127;
     }
   }
   __syncthreads();  // LDS tables initialised
