@@ -1333,46 +1333,29 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   }
   __syncthreads();
   uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
-  const uint32_t lane = lane_id();
-  // every lane of the wave calls place (valid: it holds a point).  Points of the
-  // tile's LDS entries reserve their slots wave-aggregated: one LDS atomic per
-  // distinct entry in the wave (a wave's points mostly border a few pairs), not
-  // one per point on the same few counters
-  auto place = [&](uint64_t key, bool valid) {
+  auto place = [&](uint64_t key) {
     const uint64_t r01 = key >> 24;
+    uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
     uint32_t e = 0xffffffffu;
-    if (valid) {
-      uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
-      for (int probe = 0; probe < 2 * kGrpEnt; probe++) {
-        const uint64_t k = s_hk[h];
-        if (k == r01) { e = s_he[h]; break; }
-        if (k == 0) break;
-        h = (h + 1) & (2 * kGrpEnt - 1);
-      }
+    for (int probe = 0; probe < 2 * kGrpEnt; probe++) {
+      const uint64_t k = s_hk[h];
+      if (k == r01) { e = s_he[h]; break; }
+      if (k == 0) break;
+      h = (h + 1) & (2 * kGrpEnt - 1);
     }
-    const bool local = e != 0xffffffffu && s_base[e] != kGrpDrop;
-    for (uint64_t todo = __ballot(local); todo;) {  // (uniform)
-      const int leader = __builtin_ctzll(todo);
-      const uint32_t el = wave_read(e, leader);
-      const uint64_t m = __ballot(local && e == el);
-      uint32_t base = 0;
-      if ((int)lane == leader) base = atomicAdd(&s_cur[el], (uint32_t)__popcll(m));
-      base = wave_read(base, leader);
-      if (local && e == el) grp[s_base[el] + base + lanes_below(m)] = key;
-      todo &= ~m;
-    }
-    if (valid && e == 0xffffffffu) {  // a pair missing from the tile's LDS entries (crowded tiles)
+    if (e != 0xffffffffu) {
+      if (s_base[e] == kGrpDrop) return;
+      grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = key;
+    } else {
       const uint32_t slot = ht_slot_find(ht_key, r01);
       if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) return;
       grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = key;
     }
   };
 #pragma unroll
-  for (int k = 0; k < kGrpPre; k++) place(pv[k], (uint32_t)(tid + 256 * k) < n);
-  for (uint32_t i0 = 256 * kGrpPre; i0 < n; i0 += 256) {  // (uniform trip count)
-    const uint32_t i = i0 + (uint32_t)tid;
-    place(i < n ? pts[i] : 0, i < n);
-  }
+  for (int k = 0; k < kGrpPre; k++)
+    if ((uint32_t)(tid + 256 * k) < n) place(pv[k]);
+  for (uint32_t i = tid + 256 * kGrpPre; i < n; i += 256) place(pts[i]);
 }
 
 // ---------------------------------------------------------------------------
