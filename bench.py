@@ -194,7 +194,8 @@ def main():
     assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
     scatter = args.ingest == "scatter"
     frames = render_pool(args, rank)
-    copies = 1 if args.ingest == "scatter" else max(1, args.hbm_copies)
+    # scatter: rank 0's pool per rank holds at least one batch (the pool repeated)
+    copies = -(-B // args.pool) if scatter else max(1, args.hbm_copies)
     d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
@@ -207,7 +208,7 @@ def main():
         if rank == 0:
             root_pool = torch.empty((world, npool) + frames.shape[1:], dtype=torch.uint8, device="cuda")
             for r in range(world):
-                root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames)
+                root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames).repeat(copies, 1, 1)
         ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
         rec_cap = 32  # detection records per frame gathered to rank 0 (fixed capacity)
         rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)

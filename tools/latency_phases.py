@@ -1,0 +1,34 @@
+"""Per-phase average time of the blob and decode kernels (AT_PHASE_PROBE=1) at a
+given batch size: ticks accumulated per phase over every item (wall_clock64,
+100 MHz) divided by the item count of the phase.  Usage: python tools/latency_phases.py [B]"""
+import os
+import sys
+
+import numpy as np
+
+os.environ.setdefault("AT_PHASE_PROBE", "1")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import ros_vision_amd as rva  # noqa: E402
+from ros_vision_amd import synth  # noqa: E402
+
+W, H = 1280, 720
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+frames = np.stack([synth.stream_frame(W, H, f)[0] for f in range(B)])
+d_frames = torch.from_numpy(frames).cuda()
+det = rva.GpuDetector(W, H, max_batch=B)
+for rep in range(3):
+    det.detect_device(d_frames.data_ptr(), frames[0].nbytes, B)
+p = det.copy_probe().astype(np.int64)
+for name, base in (("k_blob_small", 64), ("k_blob", 80), ("k_decode", 128)):
+    row = []
+    for k in range(1, 10):
+        t, n = p[base + k], p[base + 32 + k]
+        if n:
+            row.append("%d:%.2fus(x%d)" % (k, t / n / 100.0, n))
+    print(name, " ".join(row))
+print("pose phases (us): polar3 %.2f  OI-1 %.2f  ambiguity %.2f  OI-2 %.2f" % tuple(np.diff(p[16:21]) / 100.0))
+a = p[16 + 2]
+print("ambiguity detail (us): setup %.2f  deg2 %.2f  deg3 %.2f  deg4 %.2f  minima %.2f  rest %.2f" % (
+    (p[26] - a) / 100.0, (p[27] - p[26]) / 100.0, (p[28] - p[27]) / 100.0, (p[29] - p[28]) / 100.0,
+    (p[30] - p[29]) / 100.0, (p[19] - p[30]) / 100.0))
