@@ -386,7 +386,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.pts = (uint64_t*)dalloc(B * ntb * (size_t)g.bnd_region * 8);
   b.tcnt = (uint32_t*)dalloc(B * ntb * 4);
   b.tent = (uint32_t*)dalloc(B * ntb * 4);
-  b.grp = (uint64_t*)dalloc(B * g.cap_pts * 8);
+  b.grp = (uint32_t*)dalloc(B * g.cap_pts * 4);
+  b.keys = (uint64_t*)dalloc(B * g.cap_pts * 8);
   b.pent_key = (uint64_t*)dalloc(B * ntb * kLdsPairSlots * 8);
   b.pent_cnt = (uint32_t*)dalloc(B * ntb * kLdsPairSlots * 4);
   b.povf_key = (uint64_t*)dalloc(B * kPairEntCap * 8);
@@ -1221,7 +1222,7 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       size_t o = 0;
       for (uint32_t i = 0; i < npairs; i++) {
         if (!sel[i]) continue;
-        if (hipMemcpy((uint8_t*)dst + o * 8, d->d.grp + (size_t)frame * g.cap_pts + off[i], cnt[i] * 8,
+        if (hipMemcpy((uint8_t*)dst + o * 8, d->d.keys + (size_t)frame * g.cap_pts + off[i], cnt[i] * 8,
                       hipMemcpyDeviceToHost) != hipSuccess)
           return AT_E_HIP;
         o += cnt[i];

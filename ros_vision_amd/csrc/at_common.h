@@ -166,9 +166,8 @@ struct DevDetection {
   double pose_err[2];  // errors of the first / second minimum (HUGE_VAL: none)
 };
 
-// Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode;
-// every kept blob reserves a slot, frame == kQuadInvalid marks a rejected quad.
-constexpr uint32_t kQuadInvalid = 0xffffffffu;
+// Accepted quad (corners after AdjustPixelCenters) queued for RefineEdges + decode
+// (the blob kernels append accepted quads only, through the per-frame counter).
 struct QuadCand {
   uint32_t frame, rank;
   float p[4][2];
@@ -200,7 +199,10 @@ struct DevBufs {
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile
   uint32_t* tent;     // [B][ntb]        pair entries of each tile
-  uint64_t* grp;      // [B][cap_pts]   boundary points grouped by pair rank
+  uint32_t* grp;      // [B][cap_pts]   boundary points grouped by pair rank: the low 24 bits of the
+                      //                point key, (x << 14) | (y << 4) | (b2w << 3) | dxy
+  uint64_t* keys;     // [B][cap_pts]   k_extents' (theta, plane, y, x | W) sort keys, same slots as grp
+                      //                (and the blob kernels' IndexPoint parity tap)
   uint64_t* pent_key; // [B][ntb][kLdsPairSlots] per-tile pair histogram entries (rep01)
   uint32_t* pent_cnt; // [B][ntb][kLdsPairSlots]
   uint64_t* povf_key; // [B][kPairEntCap] entries of tiles whose LDS pair table overflowed

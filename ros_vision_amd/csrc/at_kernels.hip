@@ -192,6 +192,43 @@ __constant__ float c_filter[7] = {0.01110899634659290314f, 0.1353352814912796020
 // (8x8 full-resolution pixels).  YUYV rows are read as 16-byte loads, so a
 // wave reads 1 KiB contiguous per row.
 // ---------------------------------------------------------------------------
+// Y of the 8 full-resolution pixels (row, x .. x + 7) of a frame in format FMT
+// (0 YUYV: one 16-B load; 1 BGR8: three 8-B loads, OpenCV BGR2YUV_YUYV luma with
+// ITUR_BT_601_SHIFT 20; 2 GRAY8: one 8-B load).  x is a multiple of 8.
+template <int FMT>
+__device__ __forceinline__ void load_y8(const uint8_t* in, int W, int row, int x, uint32_t (&y)[8]) {
+  if (FMT == 0) {  // YUYV: Y at even bytes
+    const uint4 v = *reinterpret_cast<const uint4*>(in + ((size_t)row * W + x) * 2);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      y[2 * k] = w[k] & 0xff;
+      y[2 * k + 1] = (w[k] >> 16) & 0xff;
+    }
+  } else if (FMT == 1) {
+    const uint8_t* p = in + ((size_t)row * W + x) * 3;
+    const uint2 v0 = *reinterpret_cast<const uint2*>(p);
+    const uint2 v1 = *reinterpret_cast<const uint2*>(p + 8);
+    const uint2 v2 = *reinterpret_cast<const uint2*>(p + 16);
+    uint8_t bytes[24];
+    *reinterpret_cast<uint2*>(bytes) = v0;
+    *reinterpret_cast<uint2*>(bytes + 8) = v1;
+    *reinterpret_cast<uint2*>(bytes + 16) = v2;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int bb = bytes[3 * k], gg = bytes[3 * k + 1], rr = bytes[3 * k + 2];
+      y[k] = (uint32_t)((269484 * rr + 528482 * gg + 102760 * bb + (1 << 19) + (16 << 20)) >> 20);
+    }
+  } else {
+    const uint2 v = *reinterpret_cast<const uint2*>(in + (size_t)row * W + x);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      y[k] = (v.x >> (8 * k)) & 0xff;
+      y[4 + k] = (v.y >> (8 * k)) & 0xff;
+    }
+  }
+}
+
 template <int FMT>
 __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
   const int f = blockIdx.z;
@@ -211,36 +248,7 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
   for (int r = 0; r < 8; r++) {
     const int row = ty * 8 + r;
     uint32_t y[8];
-    if (FMT == 0) {  // YUYV: Y at even bytes
-      const uint4 v = *reinterpret_cast<const uint4*>(in + ((size_t)row * g.W + x0) * 2);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        y[2 * k] = w[k] & 0xff;
-        y[2 * k + 1] = (w[k] >> 16) & 0xff;
-      }
-    } else if (FMT == 1) {  // BGR8 -> Y (OpenCV BGR2YUV_YUYV, ITUR_BT_601_SHIFT 20)
-      const uint8_t* p = in + ((size_t)row * g.W + x0) * 3;
-      const uint2 v0 = *reinterpret_cast<const uint2*>(p);
-      const uint2 v1 = *reinterpret_cast<const uint2*>(p + 8);
-      const uint2 v2 = *reinterpret_cast<const uint2*>(p + 16);
-      uint8_t bytes[24];
-      *reinterpret_cast<uint2*>(bytes) = v0;
-      *reinterpret_cast<uint2*>(bytes + 8) = v1;
-      *reinterpret_cast<uint2*>(bytes + 16) = v2;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int bb = bytes[3 * k], gg = bytes[3 * k + 1], rr = bytes[3 * k + 2];
-        y[k] = (uint32_t)((269484 * rr + 528482 * gg + 102760 * bb + (1 << 19) + (16 << 20)) >> 20);
-      }
-    } else {  // GRAY8
-      const uint2 v = *reinterpret_cast<const uint2*>(in + (size_t)row * g.W + x0);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        y[k] = (v.x >> (8 * k)) & 0xff;
-        y[4 + k] = (v.y >> (8 * k)) & 0xff;
-      }
-    }
+    load_y8<FMT>(in, g.W, row, x0, y);
     uint2 gw;
     gw.x = y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24);
     gw.y = y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24);
@@ -315,7 +323,13 @@ constexpr uint32_t kKeptBit = 0x80000000u;
 // (only those can take part in k_ccl_border's unions)
 constexpr uint32_t kTouchBit = 0x80000000u;
 
-template <int TWD>
+// PRE < 0: the tile's decimated pixels and 4x4 min/max come from k_pre's planes.
+// PRE = 0 / 1 / 2 (frame format YUYV / BGR8 / GRAY8): k_pre's work is done here --
+// the workgroup reads its tile's full-resolution rows once (gray and decimated
+// planes written for the later stages), plus the decimated samples of the
+// 8-pixel halo its filtered tile min/max needs, so there is no min/max plane,
+// no re-read of the decimated plane and one launch less.
+template <int TWD, int PRE>
 __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
   constexpr int NT = CT::NT;
@@ -336,14 +350,109 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
   if (tid == 0) s_nlr = 0;
-  kt_begin(b, 1);
-
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
-  // the tile's decimated pixels (+1 halo) are loaded together with the tile
-  // min/max: one global round trip instead of two
   constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
   uint8_t dv[kDecPer];
+  // PRE: decimated samples of rows y0-8 .. y0+35, cols x0-8 .. x0+TW+7 (the tiles
+  // of s_umn), staged over s_par (unused until the labeling)
+  constexpr int kDR = kCclTileH + 12, kDC = kCclTileW + 16;
+  static_assert(PRE < 0 || kDR * kDC <= (int)sizeof(s_par), "decimated halo must fit over s_par");
+  uint8_t(*s_dec)[kDC] = reinterpret_cast<uint8_t(*)[kDC]>(s_par);
+  if constexpr (PRE >= 0) {
+    // the batch's control block starts at zero (no memset node): nothing here
+    // reads it, every later kernel follows in stream order
+    if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      for (uint32_t w = tid; w < b.ctrl_words; w += NT) b.ctrl[w] = 0;
+      __syncthreads();
+    }
+  }
+  kt_begin(b, 1);
+  if constexpr (PRE >= 0) {
+    const uint8_t* in = b.frames[f];
+    uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
+    uint8_t* decw = b.dec + (size_t)f * g.Wd * g.Hd;
+    // (1) the tile's full-resolution rows 2y0 .. 2y0+63, cols 2x0 .. 2x0+2TW-1 in
+    // 8-pixel chunks: gray out; even rows give 4 decimated samples each
+    constexpr int kCR = 2 * kCclTileW / 8;               // chunks per full row
+    constexpr int kIn = (2 * kCclTileH * kCR + NT - 1) / NT;
+    // (2) the halo's decimated samples in 4-sample chunks (8 full pixels of an
+    // even row) over the kDR x kDC region minus the interior
+    constexpr int kHCc = kDC / 4;
+    constexpr int kHal = (kDR * kHCc + NT - 1) / NT;
+    uint32_t yin[kIn][8], yh[kHal][8];
+    // every load of both parts is issued before any is used
+#pragma unroll
+    for (int k = 0; k < kIn; k++) {
+      const int i = tid + NT * k;
+      const int row = 2 * y0 + i / kCR, x = 2 * x0 + 8 * (i % kCR);
+      if (i < 2 * kCclTileH * kCR && row < g.H && x < g.W) load_y8<PRE>(in, g.W, row, x, yin[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kHal; k++) {
+      const int i = tid + NT * k;
+      const int r = i / kHCc, cc = i % kHCc;
+      const int yd = y0 - 8 + r, xd = x0 - 8 + 4 * cc;
+      const bool interior = r >= 8 && r < 8 + kCclTileH && cc >= 2 && cc < 2 + kCclTileW / 4;
+      if (i < kDR * kHCc && !interior && yd >= 0 && yd < g.Hd && xd >= 0 && xd < g.Wd)
+        load_y8<PRE>(in, g.W, 2 * yd, 2 * xd, yh[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kIn; k++) {
+      const int i = tid + NT * k;
+      const int lr = i / kCR, row = 2 * y0 + lr, x = 2 * x0 + 8 * (i % kCR);
+      if (i < 2 * kCclTileH * kCR && row < g.H && x < g.W) {
+        const uint32_t(&y)[8] = yin[k];
+        *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x) =
+            make_uint2(y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24), y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24));
+        if ((lr & 1) == 0) {
+          const uint32_t d = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
+          *reinterpret_cast<uint32_t*>(decw + (size_t)(row >> 1) * g.Wd + (x >> 1)) = d;
+          *reinterpret_cast<uint32_t*>(&s_dec[8 + (lr >> 1)][8 + (x >> 1) - x0]) = d;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kHal; k++) {
+      const int i = tid + NT * k;
+      const int r = i / kHCc, cc = i % kHCc;
+      const int yd = y0 - 8 + r, xd = x0 - 8 + 4 * cc;
+      const bool interior = r >= 8 && r < 8 + kCclTileH && cc >= 2 && cc < 2 + kCclTileW / 4;
+      if (i < kDR * kHCc && !interior && yd >= 0 && yd < g.Hd && xd >= 0 && xd < g.Wd) {
+        const uint32_t(&y)[8] = yh[k];
+        *reinterpret_cast<uint32_t*>(&s_dec[r][4 * cc]) = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
+      }
+    }
+    __syncthreads();
+    // tile min/max of every staged tile inside the image (whole tiles: W, H % 8 == 0)
+    for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
+      const int r = i / (kTW + 4), c = i % (kTW + 4);
+      const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
+      uint32_t mn = 255, mx = 0;  // out of range: neutral for min/max
+      if (tr >= 0 && tr < g.TH && tc >= 0 && tc < g.TW) {
+#pragma unroll
+        for (int dr = 0; dr < 4; dr++) {
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(&s_dec[4 * r + dr][4 * c]);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            mn = min(mn, (w >> (8 * k)) & 0xff);
+            mx = max(mx, (w >> (8 * k)) & 0xff);
+          }
+        }
+      }
+      s_umn[r][c] = (uint8_t)mn;
+      s_umx[r][c] = (uint8_t)mx;
+    }
+#pragma unroll
+    for (int k = 0; k < kDecPer; k++) {
+      const int i = tid + NT * k;
+      const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
+      dv[k] = (i < kHR * kHC && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? s_dec[i / kHC + 7][i % kHC + 7] : 0;
+    }
+    __syncthreads();  // s_dec (over s_par) read before the labeling writes s_par
+  } else {
+  // the tile's decimated pixels (+1 halo) are loaded together with the tile
+  // min/max: one global round trip instead of two
 #pragma unroll
   for (int k = 0; k < kDecPer; k++) {
     const int i = tid + NT * k;
@@ -363,6 +472,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     s_umx[r][c] = mx;
   }
   __syncthreads();
+  }
   // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+kTH-1
   for (int i = tid; i < (kTH + 1) * (kTW + 2); i += NT) {
     const int r = i / (kTW + 2), c = i % (kTW + 2);
@@ -1332,7 +1442,7 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
   }
   __syncthreads();
-  uint64_t* grp = b.grp + (size_t)f * g.cap_pts;
+  uint32_t* grp = b.grp + (size_t)f * g.cap_pts;  // the point's low 24 key bits (labels dropped)
   auto place = [&](uint64_t key) {
     const uint64_t r01 = key >> 24;
     uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
@@ -1345,11 +1455,11 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
     if (e != 0xffffffffu) {
       if (s_base[e] == kGrpDrop) return;
-      grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = key;
+      grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = (uint32_t)key & 0xffffffu;
     } else {
       const uint32_t slot = ht_slot_find(ht_key, r01);
       if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) return;
-      grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = key;
+      grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = (uint32_t)key & 0xffffffu;
     }
   };
 #pragma unroll
@@ -2051,14 +2161,14 @@ __device__ bool wave_bucket_sort_kv(BlobShared<64, CAP>& S, uint64_t (&kv)[CAP /
 
 // keys (theta, plane, y, x) from global memory: slot t = j * 64 + lane
 template <int CAP>
-__device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* grp, int n) {
+__device__ bool wave_bucket_sort(BlobShared<64, CAP>& S, const uint64_t* keys, int n) {
   constexpr int KPL = CAP / 64;
   const uint32_t lane = lane_id();
   uint64_t kv[KPL];
 #pragma unroll
   for (int j = 0; j < KPL; j++) {
     const int t = j * 64 + (int)lane;
-    kv[j] = t < n ? grp[t] : ~0ull;
+    kv[j] = t < n ? keys[t] : ~0ull;
   }
   return wave_bucket_sort_kv<CAP>(S, kv, n);
 }
@@ -2173,14 +2283,14 @@ __device__ bool team_reg_bucket_sort_kv(BlobShared<NT, CAP>& S, uint64_t (&kv)[C
 }
 
 template <int NT, int CAP>
-__device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* grp, int n) {
+__device__ bool team_reg_bucket_sort(BlobShared<NT, CAP>& S, const uint64_t* keys, int n) {
   constexpr int KPL = CAP / NT;
   const int tid = team_rank<NT>();
   uint64_t kv[KPL];
 #pragma unroll
   for (int j = 0; j < KPL; j++) {
     const int t = j * NT + tid;
-    kv[j] = t < n ? grp[t] : ~0ull;
+    kv[j] = t < n ? keys[t] : ~0ull;
   }
   return team_reg_bucket_sort_kv<NT, CAP>(S, kv, n);
 }
@@ -2213,7 +2323,7 @@ __device__ __forceinline__ Mom6 prefix_at(const BlobShared<NT, CAP>& S, const ui
 // SIMD, costs more there than the key store and reload.)  Returns SelectBlobs'
 // decision (uniform across the wave).
 __device__ bool small_extents_keys(const DevBufs& b, const Geom& g, int f, uint32_t rank, uint32_t n,
-                                   const uint64_t* grp, uint64_t (&kv)[kSmallBlob / 64]) {
+                                   const uint32_t* grp, uint64_t (&kv)[kSmallBlob / 64]) {
   constexpr int U = kSmallBlob / 64;
   const int lane = (int)lane_id();
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
@@ -2296,7 +2406,7 @@ __device__ bool small_extents_keys(const DevBufs& b, const Geom& g, int f, uint3
 // (uniform across the team).
 template <int NT, int CAP>
 __device__ bool large_extents_keys(const DevBufs& b, const Geom& g, BlobShared<NT, CAP>& S, int f, uint32_t rank,
-                                   uint32_t n, const uint64_t* grp, uint64_t (&kv)[CAP / NT]) {
+                                   uint32_t n, const uint32_t* grp, uint64_t (&kv)[CAP / NT]) {
   constexpr int U = CAP / NT;
   const int tid = team_rank<NT>();
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
@@ -2414,7 +2524,8 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   const uint32_t rank = w & 0xffff;
   const uint32_t n = pi_.n;
   big = n > 2048;
-  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + pi_.off;
+  const uint32_t* grp = b.grp + (size_t)f * g.cap_pts + pi_.off;  // points (fused extents)
+  uint64_t* keys = b.keys + (size_t)f * g.cap_pts + pi_.off;      // k_extents' sort keys
 
   // extents, SelectBlobs and the theta keys: from k_extents, or here (FUSE)
   bool sorted = false, in_lds = false;
@@ -2450,18 +2561,18 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   if constexpr (NT == 64) {
     if (n >= 64) {  // keys go straight from global memory into registers
       phase(1);
-      sorted = wave_bucket_sort<CAP>(S, grp, (int)n);
+      sorted = wave_bucket_sort<CAP>(S, keys, (int)n);
       in_lds = true;
     }
   } else if constexpr (CAP / NT <= 16) {
     if (n >= 64) {
       phase(1);
-      sorted = team_reg_bucket_sort<NT, CAP>(S, grp, (int)n);
+      sorted = team_reg_bucket_sort<NT, CAP>(S, keys, (int)n);
       in_lds = true;
     }
   }
   if (!sorted && !in_lds) {
-    for (uint32_t t = tid; t < n; t += NT) S.keys[t] = grp[t];
+    for (uint32_t t = tid; t < n; t += NT) S.keys[t] = keys[t];
     phase(1);
     team_sync<NT>();
     sorted = team_bucket_sort<NT, CAP>(S, (int)n);
@@ -2496,7 +2607,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       // parity tap: IndexPoint key (blob, theta, point bits) in place of the grouped point
       const uint64_t pbits = (((sk >> 10) & 0x3ff) << 14) | (((sk >> 20) & 0x3ff) << 4) | (((sk >> 9) & 1) << 3) |
                              ((sk >> 30) & 3);
-      if (prm.taps) grp[t] = ((uint64_t)bi << 52) | (((sk >> kKeyTheta) & 0xfffffff) << 24) | pbits;
+      if (prm.taps) keys[t] = ((uint64_t)bi << 52) | (((sk >> kKeyTheta) & 0xfffffff) << 24) | pbits;
       mom_add(csum, point_mom(word[k]));
     }
   }
@@ -2903,7 +3014,9 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   const int f = (int)(w >> 16);
   const uint32_t rank = w & 0xffff;
   const uint32_t n = b.pair_cnt[(size_t)f * kMaxPairs + rank];
-  uint64_t* grp = b.grp + (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
+  const size_t so = (size_t)f * g.cap_pts + b.pair_off[(size_t)f * kMaxPairs + rank];
+  const uint32_t* grp = b.grp + so;
+  uint64_t* keys = b.keys + so;
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
   uint32_t mnx = 0xffff, mny = 0xffff, mxx = 0, mxy = 0;
   int32_t sgx = 0, sgy = 0;
@@ -2911,9 +3024,9 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   // U points per lane per round, every load of a round issued before any is
   // used; the first round's keys stay in registers for the key pass below
   constexpr int U = 8;
-  uint64_t kr[U];
+  uint32_t kr[U];
   for (uint32_t base = 0; base < n; base += NT * U) {
-    uint64_t kk[U];
+    uint32_t kk[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t t = base + u * NT + tid;
@@ -2965,7 +3078,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   if (tid == 0) b.pair_sel[(size_t)f * kMaxPairs + rank] = 1;
   const double cx = ext_cx(e), cy = ext_cy(e);
   for (uint32_t base = 0; base < n; base += NT * U) {
-    uint64_t kk[U];
+    uint32_t kk[U];
     uint32_t gp[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -3008,7 +3121,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
       }
       // sort key: order (theta, plane, y, x) == P6 stable order; b2w and W ride in
       // the low bits (never decide: (plane, y, x) is unique)
-      grp[t] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
+      keys[t] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
                ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
     }
   }
@@ -3273,28 +3386,10 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       t_last = now;
     }
   };
-  // static round-robin over the queue in chunks of 64 items: one load per lane
-  // finds the chunk's accepted quads (rejected ones keep an invalid slot), so a
-  // run of rejected entries costs one round trip, not one each
+  // static round-robin over the queue (every entry is an accepted quad: the blob
+  // kernels append only those)
   const uint32_t G = gridDim.x;
-  for (uint32_t base = blockIdx.x; base < nq; base += 64u * G) {
-  uint64_t vmask;
-  {
-    const uint32_t it = base + (uint32_t)tid * G;
-    bool v = false;
-    if (it < nq) {
-      int lo = 0, hi = B - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (qpre[mid] <= it) lo = mid;
-        else hi = mid - 1;
-      }
-      v = b.qcand[(size_t)lo * kQuadCandPerFrame + (it - qpre[lo])].frame != kQuadInvalid;
-    }
-    vmask = __ballot(v);
-  }
-  for (; vmask; vmask &= vmask - 1) {
-    const uint32_t item = base + (uint32_t)__builtin_ctzll(vmask) * G;
+  for (uint32_t item = blockIdx.x; item < nq; item += G) {
     int lo = 0, hi = B - 1;  // last frame whose prefix <= item
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -3302,7 +3397,6 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       else hi = mid - 1;
     }
     const QuadCand& qd = b.qcand[(size_t)lo * kQuadCandPerFrame + (item - qpre[lo])];
-    if (qd.frame == kQuadInvalid) continue;  // a kept blob whose quad UpdateFitQuads rejected (uniform)
     const int f = (int)qd.frame;
     const uint32_t qrank = qd.rank;
     const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
@@ -3629,7 +3723,6 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     phase(9);
   }
-  }
   probe_flush(b, prm, pacc, 128, tid == 0);
   if (tid == 0) kt_end(b, 10);
 }
@@ -3915,7 +4008,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     dim3 blk(64, 4), grd((g.TW + 63) / 64, (g.TH + 3) / 4, B);
     tk(0, st, 0);
-    if (!on(0)) {}
+    // latency mode: k_thr_ccl does k_pre's work (one launch less on the B = 1 chain;
+    // in throughput mode the longer k_thr_ccl costs ~6 % of concurrent throughput)
+    if (!on(0) || g.ctw == 32) {}
     else if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
     else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
     else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
@@ -3929,8 +4024,10 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     dim3 grd(g.CTX, g.CTY, B);
     tk(1, st, 0);
     if (!on(1)) {}
-    else if (g.ctw == 32) hipLaunchKernelGGL(k_thr_ccl<32>, grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
-    else hipLaunchKernelGGL(k_thr_ccl<64>, grd, dim3(CclTile<64>::NT), 0, st, b, g, prm);
+    else if (g.ctw != 32) hipLaunchKernelGGL((k_thr_ccl<64, -1>), grd, dim3(CclTile<64>::NT), 0, st, b, g, prm);
+    else if (fmt == 0) hipLaunchKernelGGL((k_thr_ccl<32, 0>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
+    else if (fmt == 1) hipLaunchKernelGGL((k_thr_ccl<32, 1>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
+    else hipLaunchKernelGGL((k_thr_ccl<32, 2>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
     tk(1, st, 1);
     mark();
     tk(2, st, 0);
@@ -3966,7 +4063,12 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   mark();
   tk(7, st, 0);
   // (latency mode: the blob kernels do k_extents' work themselves, up to 4096-point blobs)
-  if (on(7) && (g.ctw != 32 || g.max_cluster > 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
+  // latency mode: extents, SelectBlobs and keys inside the small-blob wave and (up to
+  // 4096-point blobs) the 512-thread large-blob team.  (Throughput mode keeps
+  // k_extents: the fused small-blob kernel needs 2 waves/SIMD, or spills at 4, and
+  // measured 1-5 % slower in concurrent throughput, profiles/r03h, r03i.)
+  const bool fuse_small = g.ctw == 32;
+  if (on(7) && !(g.ctw == 32 && g.max_cluster <= 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
   tk(7, st, 1);
   mark();
   auto blob_large = [&](hipStream_t s) {
@@ -3988,7 +4090,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   auto blob_small = [&](hipStream_t s) {
     tk(8, s, 0);
     if (!on(8)) {}
-    else if (g.ctw == 32) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    else if (fuse_small) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
     else hipLaunchKernelGGL(k_blob_small<false>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
     tk(8, s, 1);
   };
