@@ -113,7 +113,7 @@ using namespace at;
 // words, then scalars
 enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlPerFrame };
 enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
-       kCtlDetHead = kCtlNcls + kNumCls, kCtlScalars = kCtlDetHead + 1 };
+       kCtlDetHead = kCtlNcls + kNumCls, kCtlDecDone = kCtlDetHead + 1, kCtlScalars = kCtlDecDone + 1 };
 
 static constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 
@@ -381,6 +381,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.par = (uint32_t*)dalloc(B * nd * 4);
   b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodesMax * 4);
   b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
+  b.blink = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 8 * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
   b.pts = (uint64_t*)dalloc(B * ntb * (size_t)g.bnd_region * 8);
@@ -425,6 +426,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.blob_pts = sc + kCtlBlobPts;
   b.ncls = sc + kCtlNcls;
   b.det_head = sc + kCtlDetHead;
+  b.dec_done = sc + kCtlDecDone;
   b.kt_stage = -1;
   b.kstamp = reinterpret_cast<uint64_t*>(d->d_ctrl + d->kstamp_word);
   b.kgrid = d->d_ctrl + d->kstamp_word + 4;
@@ -1194,12 +1196,27 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
               hipSuccess)
         return AT_E_HIP;
       size_t np = 0;
-      for (size_t t = 0; t < ntb; t++) np += tc[t];
+      for (size_t t = 0; t < ntb; t++) np += tc[t] & ~kTileNarrow;
       if (bytes < np * 8) return AT_E_INVALID;
+      // narrow tiles hold (entry index, point bits) words: the key is the entry's pair
+      // key over the point bits
+      std::vector<uint64_t> ekey(ntb * (size_t)kLdsPairSlots);
+      if (hipMemcpy(ekey.data(), d->d.pent_key + frame * ntb * kLdsPairSlots, ekey.size() * 8,
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        return AT_E_HIP;
       size_t o = 0;
       for (size_t t = 0; t < ntb; t++) {
-        memcpy((uint8_t*)dst + o * 8, all.data() + t * g.bnd_region, tc[t] * 8);
-        o += tc[t];
+        const uint32_t n = tc[t] & ~kTileNarrow;
+        if (tc[t] & kTileNarrow) {
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(all.data() + t * g.bnd_region);
+          for (uint32_t i = 0; i < n; i++) {
+            const uint64_t key = (ekey[t * kLdsPairSlots + (w[i] >> 23)] << 24) | ((w[i] & 0x7ffffcu) << 1) | (w[i] & 3u);
+            memcpy((uint8_t*)dst + (o + i) * 8, &key, 8);
+          }
+        } else {
+          memcpy((uint8_t*)dst + o * 8, all.data() + t * g.bnd_region, (size_t)n * 8);
+        }
+        o += n;
       }
       return (long long)(np * 8);
     }

@@ -37,6 +37,8 @@ constexpr int kBndRows = 4;
 constexpr int kBndPts = 64 * 4 * kBndRows * 4;  // worst case: 4 points per pixel (global region per tile)
 constexpr int kBndStage = 1024;                 // of which staged in LDS (1 per pixel; typical tiles hold ~0.7)
 constexpr int kLdsPairSlots = 512;
+// tcnt flag: the tile's points are 4-B (entry index, point bits) words (k_boundary)
+constexpr uint32_t kTileNarrow = 0x80000000u;
 constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
@@ -195,6 +197,7 @@ struct DevBufs {
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
   uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodesMax] local roots of each CCL tile (global node ids)
   uint32_t* nlroot;   // [B][CTX*CTY]
+  uint32_t* blink;    // [B][CTX*CTY][8] k_thr_ccl's mask of the tile's border candidates that link
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile
@@ -221,6 +224,7 @@ struct DevBufs {
   DevDetection* dets; // [det_cap] batch-wide pool of candidates (DevDetection::frame)
   uint32_t det_cap;
   uint32_t* det_head; // [1] pool cursor (control block)
+  uint32_t* dec_done; // [1] finished k_decode workgroups (control block; latency mode's fused pose)
   // zero-copy results: the detections (k_decode, poses added by k_pose) and the
   // control block (copied by k_pose) are also written straight into the
   // caller-visible pinned host buffers (device pointers of mapped host memory),

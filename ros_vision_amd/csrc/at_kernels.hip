@@ -316,6 +316,17 @@ __device__ __forceinline__ uint32_t slot_of(int ty, int tx, int type) {
   return (uint32_t)(ty * T::ROW_NODES + (type == 0 ? tx : T::BW + 2 * tx + (type - 1)));
 }
 
+// One candidate union per thread (the reference's Merge, labeling_allegretti_2019_BKE.cu:302-338,
+// over the tile's border blocks): threads 0..5*BW-1 the top block row (BW blocks x
+// P, Q, R and the two background links), then the left block column (BH x P, S,
+// background S), then the right column (BH-1 x R).  Every union is one short
+// chain of global round trips instead of up to five in a row per lane.
+template <int TW>
+struct BorderRoles {
+  static constexpr int Top = 5 * CclTile<TW>::BW, Left = 3 * CclTile<TW>::BH, Right = CclTile<TW>::BH - 1;
+  static constexpr int NT = (Top + Left + Right + 63) / 64 * 64;
+};
+
 // kept bit of a root's parent word: the component has >= 25 pixels (BlobDiff's
 // size test, apriltag_gpu.cu:331-337), throughput mode
 constexpr uint32_t kKeptBit = 0x80000000u;
@@ -349,7 +360,9 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint32_t s_par[kCclTileNodes];
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
+  __shared__ uint32_t s_blink[8];  // this tile's k_ccl_border candidates that link (one bit per thread)
   if (tid == 0) s_nlr = 0;
+  if (tid < 8) s_blink[tid] = 0;
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
@@ -553,6 +566,34 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       hL = ((sr >> hl) & 1) ? slot_of<TWD>(bty, btx - (lane - hl), 2) : slot_of<TWD>(bty, btx - (lane - hl), 1);
     }
     hR = bg_in ? hL : R;
+    {
+      // k_ccl_border's link tests across the tile's top row / left and right columns
+      // (the reference's Merge conditions) on the threshold halo already in LDS: a
+      // bit per candidate, so that kernel reads one mask instead of the threshold plane
+      using BR = BorderRoles<TWD>;
+      const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
+      if (BY < g.BH && BX < g.BW && BY > 0 && bty == 0) {
+        const uint32_t m = (uint32_t)(a == 255 && T(pr - 1, pc - 1) == 255) |
+                           ((uint32_t)((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255)) << 1) |
+                           ((uint32_t)(bb == 255 && T(pr - 1, pc + 2) == 255) << 2) |
+                           ((uint32_t)(a == 0 && T(pr - 1, pc) == 0) << 3) | ((uint32_t)(bb == 0 && T(pr - 1, pc + 1) == 0) << 4);
+        for (int k = 0; k < 5; k++)
+          if ((m >> k) & 1) atomicOr(&s_blink[(btx * 5 + k) >> 5], 1u << ((btx * 5 + k) & 31));
+      }
+      if (BY < g.BH && BX < g.BW && BX > 0 && btx == 0) {
+        const uint32_t m = (uint32_t)(BY > 0 && bty > 0 && a == 255 && T(pr - 1, pc - 1) == 255) |
+                           ((uint32_t)((a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255)) << 1) |
+                           ((uint32_t)((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0)) << 2);
+        for (int k = 0; k < 3; k++) {
+          const int t = BR::Top + bty * 3 + k;
+          if ((m >> k) & 1) atomicOr(&s_blink[t >> 5], 1u << (t & 31));
+        }
+      }
+      if (BY < g.BH && BX < g.BW && BY > 0 && btx == kCclBW - 1 && bty >= 1 && bb == 255 && T(pr - 1, pc + 2) == 255) {
+        const int t = BR::Top + BR::Left + bty - 1;
+        atomicOr(&s_blink[t >> 5], 1u << (t & 31));
+      }
+    }
     s_par[F] = hF;
     s_par[L] = hL;
     s_par[R] = hR;
@@ -640,6 +681,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     if (cR && (wR & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
+  if (tid < 8) b.blink[((size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x) * 8 + tid] = s_blink[tid];
   if (tid == 0) {
     b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
     kt_end(b, 1);
@@ -705,16 +747,6 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
   }
 }
 
-// One candidate union per thread (the reference's Merge, labeling_allegretti_2019_BKE.cu:302-338,
-// over the tile's border blocks): threads 0..5*BW-1 the top block row (BW blocks x
-// P, Q, R and the two background links), then the left block column (BH x P, S,
-// background S), then the right column (BH-1 x R).  Every union is one short
-// chain of global round trips instead of up to five in a row per lane.
-template <int TW>
-struct BorderRoles {
-  static constexpr int Top = 5 * CclTile<TW>::BW, Left = 3 * CclTile<TW>::BH, Right = CclTile<TW>::BH - 1;
-  static constexpr int NT = (Top + Left + Right + 63) / 64 * 64;
-};
 template <int TWD>
 __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, Geom g) {
   constexpr int kBorderTop = BorderRoles<TWD>::Top, kBorderLeft = BorderRoles<TWD>::Left,
@@ -731,40 +763,26 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
   }
   const int BY = blockIdx.y * kCclBH + bty, BX = blockIdx.x * kCclBW + btx;
   if (BY >= g.BH || BX >= g.BW) role = 3;
-  const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
+  // which candidates link: k_thr_ccl's mask of this tile (one round trip, no
+  // threshold reads); the node pair of each candidate follows from its role
+  const uint32_t* bl = b.blink + ((size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x) * 8;
+  const bool link = role != 3 && ((bl[t >> 5] >> (t & 31)) & 1u);
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
   const int Wd = g.Wd;
-  const int row = 2 * BY, col = 2 * BX;
-  const size_t idx = (size_t)row * Wd + col;
-  auto px = [&](int r, int c) -> uint8_t {
-    if (r < 0 || c < 0 || r >= g.Hd || c >= g.Wd) return 127;
-    return thr[(size_t)r * Wd + c];
-  };
-  const bool act = role != 3;  // (no loads outside the image for the padding threads)
-  const uint8_t a = act ? thr[idx] : 127, bb = act ? thr[idx + 1] : 127, c = act ? thr[idx + Wd] : 127;
-  const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
-  uint32_t u = 0, v = 0;
-  bool link = false;
-  if (role == 0 && BY > 0) {
-    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
-    else if (kind == 1) {
-      link = (a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255);
-      u = F; v = F - 2 * Wd;
-    }
-    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2; }
-    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - 2 * Wd; }
-    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - 2 * Wd; }
-  } else if (role == 1 && BX > 0) {
-    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
-    else if (kind == 1) {
-      link = (a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255);
-      u = F; v = F - 2;
-    } else {
-      link = (a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0);
-      u = L; v = L - 1;
-    }
-  } else if (role == 2 && BY > 0) {
-    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
+  const uint32_t F = (uint32_t)((2 * BY) * Wd + 2 * BX), L = F + (uint32_t)Wd, R = L + 1;
+  uint32_t u = F, v = 0;
+  if (role == 0) {
+    if (kind == 0) v = F - 2 * Wd - 2;
+    else if (kind == 1) v = F - 2 * Wd;
+    else if (kind == 2) v = F - 2 * Wd + 2;
+    else if (kind == 3) { u = L; v = L - 2 * Wd; }
+    else { u = R; v = R - 2 * Wd; }
+  } else if (role == 1) {
+    if (kind == 0) v = F - 2 * Wd - 2;
+    else if (kind == 1) v = F - 2;
+    else { u = L; v = L - 1; }
+  } else {
+    v = F - 2 * Wd + 2;
   }
   if (link) g_union2(par, u, v);
   if (b.kt_stage == 2) {  // (uniform: the timed launch only)
@@ -885,6 +903,22 @@ __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uin
   return false;
 }
 
+// slot of a key already in the tile's LDS pair table
+__device__ __forceinline__ uint32_t lds_pair_slot(const uint64_t* keys, uint64_t key) {
+  uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
+  while (keys[h] != key) h = (h + 1) & (kLdsPairSlots - 1);
+  return h;
+}
+
+// Narrow tile points (tcnt flag kTileNarrow): 4-B words, the tile's pair-entry
+// index (9 bits) over the point bits of the key -- x (10), y (10), b2w, dxy (2):
+// the labels are the entry's key (pent_key), so they need not travel per point.
+__device__ __forceinline__ uint32_t narrow_point(uint32_t entry, uint64_t key) {
+  return (entry << 23) | ((uint32_t)(key >> 1) & 0x7ffffcu) | ((uint32_t)key & 3u);
+}
+// ... and back to the low 24 key bits (x << 14 | y << 4 | b2w << 3 | dxy)
+__device__ __forceinline__ uint32_t narrow_bits(uint32_t w) { return ((w & 0x7ffffcu) << 1) | (w & 3u); }
+
 // One 256-thread workgroup covers a 64 x (4*kBndRows) tile of interior pixels.
 // Points are staged in LDS (wave-aggregated LDS atomics) and written out with
 // ONE global atomic per workgroup; the pair histogram is aggregated in an LDS
@@ -912,7 +946,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   // pixel); the rare denser tile writes the excess straight to its global
   // region.  Keeping the stage small keeps 6 workgroups (24 waves) per CU.
   __shared__ uint64_t s_pts[kBndStage];
-  __shared__ uint32_t s_npts, s_nent;
+  __shared__ uint32_t s_npts, s_nent, s_spill;
   // threshold values with pixels of blobs under 25 pixels folded to 127: every
   // BlobDiff condition then reads one byte per neighbour (v0 + v1 == 255 holds
   // only when both blobs are kept; the dedup rule's "!= 127 and kept" likewise)
@@ -925,7 +959,7 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
     s_pkey[i] = 0;
     s_pcnt[i] = 0;
   }
-  if (tid == 0) { s_npts = 0; s_nent = 0; }
+  if (tid == 0) { s_npts = 0; s_nent = 0; s_spill = 0; }
   // stage the tile's threshold values and labels (+1 halo: rows y0..y0+16, cols
   // x0-1..x0+64) and, per pixel, whether its blob has >= 25 pixels: two
   // dependent global round trips per workgroup, then the point logic runs on LDS
@@ -1008,7 +1042,10 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       const uint64_t same_mask = __ballot(same);
       if (has && !same) {
         const uint32_t len = run_len(same_mask, lane);
-        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) bnd_spill(b, f, r01, len);  // LDS table full
+        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) {  // LDS table full
+          bnd_spill(b, f, r01, len);
+          s_spill = 1;
+        }
       }
     }
     // wave-aggregated append of the points into the LDS staging buffer
@@ -1030,21 +1067,36 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
   // (no per-frame counter: a device-scope atomic per tile on a per-frame
   // address serialized the tiles of a frame)
   const uint32_t total = s_npts;
-  const uint32_t staged = total < (uint32_t)kBndStage ? total : (uint32_t)kBndStage;
-  for (uint32_t i = tid; i < staged; i += 256) pts_out[i] = s_pts[i];
+  // narrow tile: every point staged and every pair in the LDS table -> 4-B points
+  // carrying their entry index (half the bytes for k_group, which then needs no
+  // key lookup); otherwise the 8-B keys
+  const bool narrow = total <= (uint32_t)kBndStage && !s_spill;
   uint64_t* ekey = b.pent_key + tb * kLdsPairSlots;
   uint32_t* ecnt = b.pent_cnt + tb * kLdsPairSlots;
+  uint32_t* s_ent = s_tlab;  // slot -> entry index (the label table is dead)
   for (int i = tid; i < kLdsPairSlots; i += 256) {
     const uint64_t k = s_pkey[i];
     if (k) {
       const uint32_t o = atomicAdd(&s_nent, 1u);
       ekey[o] = k;
       ecnt[o] = s_pcnt[i];
+      s_ent[i] = o;
     }
+  }
+  if (narrow) {
+    __syncthreads();
+    uint32_t* out = reinterpret_cast<uint32_t*>(pts_out);
+    for (uint32_t i = tid; i < total; i += 256) {
+      const uint64_t k = s_pts[i];
+      out[i] = narrow_point(s_ent[lds_pair_slot(s_pkey, k >> 24)], k);
+    }
+  } else {
+    const uint32_t staged = total < (uint32_t)kBndStage ? total : (uint32_t)kBndStage;
+    for (uint32_t i = tid; i < staged; i += 256) pts_out[i] = s_pts[i];
   }
   __syncthreads();
   if (tid == 0) {
-    b.tcnt[tb] = min(total, (uint32_t)g.bnd_region);
+    b.tcnt[tb] = min(total, (uint32_t)g.bnd_region) | (narrow ? kTileNarrow : 0u);
     b.tent[tb] = s_nent;
     kt_end(b, 4);
   }
@@ -1146,7 +1198,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     // every entry of the frame in one flat pass
     // thread t owns tile t (ntb <= kMaxTilesPerFrame = 1024)
     const uint32_t ne = tid < ntb ? b.tent[(size_t)f * ntb + tid] : 0u;
-    const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] : 0u;
+    const uint32_t np = tid < ntb ? b.tcnt[(size_t)f * ntb + tid] & ~kTileNarrow : 0u;
     const uint32_t incl_e = block_incl_scan(ne, s_wsum, &tot_e, 16);
     if (tid < ntb) s_tpre[tid] = incl_e - ne;
     if (tid == 0) s_tpre[ntb] = tot_e;
@@ -1404,9 +1456,12 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const int tid = threadIdx.x;
   const size_t tb = (size_t)f * g.ntb + blockIdx.x;
   const uint64_t* pts = b.pts + tb * g.bnd_region;
-  // one round trip: status, counters, entry, points
+  // one round trip: status, counters, entry, points (the first 512 8-B keys or
+  // 1024 narrow words: the same bytes)
   const uint32_t st = b.status[f];
-  const uint32_t n = b.tcnt[tb], ne = b.tent[tb];
+  const uint32_t tc = b.tcnt[tb], ne = b.tent[tb];
+  const uint32_t n = tc & ~kTileNarrow;
+  const bool narrow = (tc & kTileNarrow) != 0;
   uint64_t ekey = 0;
   uint32_t ebase = kGrpFallback;
   if (tid < kGrpEntPre) {
@@ -1426,6 +1481,38 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const uint32_t* ht_cnt = b.ht_cnt + (size_t)f * kHashSlots;
   uint32_t* ht_cur = b.ht_cur + (size_t)f * kHashSlots;
   auto in_bounds = [&](uint32_t c) { return c >= g.min_cluster && c <= g.max_cluster; };
+  uint32_t* grp = b.grp + (size_t)f * g.cap_pts;  // the point's low 24 key bits (labels dropped)
+  // a point whose entry has no LDS cursor (the tile's entries past kGrpEnt, or an
+  // LDS table overflow in k_boundary) reserves its slot in the frame's pair table
+  auto place_global = [&](uint64_t r01, uint32_t bits) {
+    const uint32_t slot = ht_slot_find(ht_key, r01);
+    if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) return;
+    grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = bits;
+  };
+  if (narrow) {
+    // the words carry their entry index: entry -> base and cursor in LDS, no lookup
+    if (tid < kGrpEnt && (uint32_t)tid < ne) {
+      s_base[tid] = ebase;
+      s_cur[tid] = 0;
+    }
+    __syncthreads();
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(pts);
+    auto place = [&](uint32_t w) {
+      const uint32_t e = w >> 23;
+      const uint32_t base = e < (uint32_t)kGrpEnt ? s_base[e] : kGrpFallback;
+      if (base == kGrpDrop) return;
+      if (base != kGrpFallback) grp[base + atomicAdd(&s_cur[e], 1u)] = narrow_bits(w);
+      else place_global(b.pent_key[tb * kLdsPairSlots + e], narrow_bits(w));
+    };
+#pragma unroll
+    for (int k = 0; k < kGrpPre; k++) {
+      const uint32_t i = 2 * (tid + 256 * k);
+      if (i < n) place((uint32_t)pv[k]);
+      if (i + 1 < n) place((uint32_t)(pv[k] >> 32));
+    }
+    for (uint32_t i = tid + 512 * kGrpPre; i < n; i += 256) place(pw[i]);
+    return;
+  }
   for (int i = tid; i < 2 * kGrpEnt; i += 256) s_hk[i] = 0;
   __syncthreads();
   if (tid < kGrpEnt && (uint32_t)tid < ne && ebase != kGrpFallback) {
@@ -1442,7 +1529,6 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
   }
   __syncthreads();
-  uint32_t* grp = b.grp + (size_t)f * g.cap_pts;  // the point's low 24 key bits (labels dropped)
   auto place = [&](uint64_t key) {
     const uint64_t r01 = key >> 24;
     uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
@@ -1457,9 +1543,7 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
       if (s_base[e] == kGrpDrop) return;
       grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = (uint32_t)key & 0xffffffu;
     } else {
-      const uint32_t slot = ht_slot_find(ht_key, r01);
-      if (slot == 0xffffffffu || !in_bounds(ht_cnt[slot])) return;
-      grp[ht_off[slot] + atomicAdd(ht_cur + slot, 1u)] = (uint32_t)key & 0xffffffu;
+      place_global(r01, (uint32_t)key & 0xffffffu);
     }
   };
 #pragma unroll
@@ -3182,12 +3266,17 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
 }
 
 // K9a (large blobs, > kSmallBlob points): one blob per NT-thread workgroup
-// iteration, persistent over the large work list.
+// iteration, persistent over the large work list.  Geometries whose blobs can
+// exceed 4096 points (max_cluster = 2 (W + H) > 4096, e.g. 1080p) run two
+// launches: CAP 4096 (49 KB LDS) over the items of up to 4096 points and CAP
+// 8192 (86 KB, one workgroup per CU) over the few larger ones (nlo = 4096,
+// size class 0 only, its own dequeue head), instead of every large blob in
+// the 86 KB kernel.
 template <int NT, int CAP, bool FUSE = false>
-__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
+__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
-  kt_begin(b, 9);
+  if (!nlo) kt_begin(b, 9);  // (the device-clock span times the first launch)
   uint32_t* pacc = S.pacc;
   if (tid < 22) pacc[tid] = 0;
   if (tid == 0) S.slow_dt = 0;
@@ -3196,26 +3285,30 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm) {
   load_combos(s_combo, tid, NT);
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
   __syncthreads();
+  const int ncls = nlo ? 1 : kNumLargeCls;  // (blobs over 4096 points are all in class 0)
   uint32_t nwork = 0;
-  for (int c = 0; c < kNumLargeCls; c++) nwork += s_cnt[c];
+  for (int c = 0; c < ncls; c++) nwork += s_cnt[c];
+  uint32_t* head = nlo ? b.workhead_small : b.workhead;
   // dynamic dequeue over the size-ordered list (longest first): large blobs
   // vary 8x in cost, and there are few of them, so one atomic per item is cheap
   while (true) {
-    if (tid == 0) S.item = atomicAdd(b.workhead, 1u);
+    if (tid == 0) S.item = atomicAdd(head, 1u);
     __syncthreads();
     const uint32_t item = S.item;
     __syncthreads();
     if (item >= nwork) break;
     uint32_t w = 0;
-    work_item(b, s_cnt, 0, kNumLargeCls, item, &w);
-    blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w), pacc);
+    work_item(b, s_cnt, 0, ncls, item, &w);
+    const PairInfo pi = FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w);
+    if (pi.n > (uint32_t)CAP || pi.n <= nlo) continue;  // the other launch's item (uniform)
+    blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, pi, pacc);
   }
   __syncthreads();
   probe_flush(b, prm, pacc, 80, tid == 0);
   probe_flush_slow(b, prm, S, tid == 0);
   if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
   if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
-  if (tid == 0) kt_end(b, 9);
+  if (tid == 0 && !nlo) kt_end(b, 9);
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
@@ -3339,14 +3432,84 @@ struct DecodeShared {
   uint32_t qpre[kMaxBatch + 1];
 };
 
+// POSE: the decode wave's hand-over to the pose wave (LDS): the homography and
+// unrotated corners of quad `seq`, and the pose the pose wave acknowledges with `ack`
+struct PoseHandoff {
+  double H[9], p[4][2];
+  double R[9], t[3], err[2];
+  uint32_t seq, ack, exit;
+};
+__device__ void pose_worker(PoseHandoff& P, const Params& prm) {
+  const uint32_t lane = lane_id();
+  uint32_t seen = 0;
+  while (true) {
+    uint32_t sq;
+    bool done = false;
+    while ((sq = __hip_atomic_load(&P.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == seen) {
+      // (the decode wave raises exit only after the last pose was acknowledged)
+      if (__hip_atomic_load(&P.exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { done = true; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (done) return;
+    seen = sq;
+    double H[9], pc[4][2];
+#pragma unroll
+    for (int k = 0; k < 9; k++) H[k] = P.H[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { pc[k][0] = P.p[k][0]; pc[k][1] = P.p[k][1]; }
+    double R[9], t[3], err[2];
+    pose::estimate_tag_pose<true>(H, pc, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, (int)(lane & 3));
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) P.R[k] = R[k];
+#pragma unroll
+      for (int k = 0; k < 3; k++) P.t[k] = t[k];
+      P.err[0] = err[0];
+      P.err[1] = err[1];
+      __hip_atomic_store(&P.ack, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+// POSE: the last decode workgroup to finish copies the (final) control block to
+// the caller-visible host buffer (k_pose's job in the unfused sequence)
+__device__ void decode_finish(const DevBufs& b, int lane) {
+  uint32_t last = 0;
+  if (lane == 0) {
+    __threadfence();
+    last = atomicAdd(b.dec_done, 1u) == gridDim.x - 1;
+  }
+  last = __shfl(last, 0);
+  if (!last) return;
+  __threadfence();
+  for (uint32_t w = (uint32_t)lane; w < b.ctrl_words; w += 64)
+    b.hctrl[w] = __hip_atomic_load(b.ctrl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 #ifndef AT_DEC_WAVES
 #define AT_DEC_WAVES 2
 #endif
-__global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(AT_DEC_WAVES))) void k_decode(DevBufs b, Geom g, Params prm, int B) {
+// POSE (latency mode, tag_size > 0): a second wave per workgroup estimates the
+// tag pose (k_pose's work) of every quad as soon as its homography is known,
+// while the first wave decodes the bits; the pose is computed on the unrotated
+// homography and corners and rotated with the decoded orientation afterwards
+// (R = R0 Rz(rot), t = t0: the corner correspondence of a 90-degree turn of
+// the tag frame), so the B = 1 chain is homography + pose instead of decode +
+// pose.  The last workgroup to finish hands the control block to the host.
+template <bool POSE>
+__global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_waves_per_eu(POSE ? 1 : AT_DEC_WAVES))) void k_decode(DevBufs b, Geom g, Params prm, int B) {
   constexpr int RCAP = kMaxRefineSamples;
   __shared__ DecodeShared S;
+  __shared__ PoseHandoff P;
   const int tid = threadIdx.x;
   kt_begin(b, 10);
+  if (POSE) {
+    if (tid == 0) { P.seq = 0; P.ack = 0; P.exit = 0; }
+    __syncthreads();
+    if (tid >= 64) {
+      pose_worker(P, prm);
+      return;
+    }
+  }
   double* gsx = b.rsamp + (size_t)blockIdx.x * (2 * (kMaxRefineSamples - kLdsRefine));
   double* gsy = gsx + (kMaxRefineSamples - kLdsRefine);
   // exclusive prefix of the per-frame candidate counts: item -> (frame, index)
@@ -3370,9 +3533,12 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
     }
     if (tid == 63) qpre[B] = incl;
   }
-  for (int i = tid; i < prm.fam.ncodes; i += kDecodeThreads) S.book[i] = b.book_code[i];
-  __syncthreads();
+  team_sync<64>();
   const uint32_t nq = qpre[B];
+  if (blockIdx.x < nq) {  // (workgroups without a quad skip the codebook)
+    for (int i = tid; i < prm.fam.ncodes; i += kDecodeThreads) S.book[i] = b.book_code[i];
+    team_sync<64>();
+  }
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[128 + k], counts [160 + k])
   uint32_t pacc[21] = {0};
   uint64_t t_last = 0;
@@ -3389,6 +3555,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
   // static round-robin over the queue (every entry is an accepted quad: the blob
   // kernels append only those)
   const uint32_t G = gridDim.x;
+  uint32_t pose_seq = 0;  // (POSE) quads handed to the pose wave
   for (uint32_t item = blockIdx.x; item < nq; item += G) {
     int lo = 0, hi = B - 1;  // last frame whose prefix <= item
     while (lo < hi) {
@@ -3401,7 +3568,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
     const uint32_t qrank = qd.rank;
     const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
     if (tid < 4) { S.qc[tid][0] = qd.p[tid][0]; S.qc[tid][1] = qd.p[tid][1]; }
-    __syncthreads();
+    team_sync<64>();
     phase(0);
     if (prm.refine_edges) {
       if (tid < 4) {
@@ -3416,12 +3583,12 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
         S.enx[tid] = nx;
         S.eny[tid] = ny;
       }
-      __syncthreads();
+      team_sync<64>();
       if (tid == 0) {
         int acc = 0;
         for (int k = 0; k < 4; k++) { S.samp_off[k] = acc; acc += S.nsamp[k]; }
       }
-      __syncthreads();
+      team_sync<64>();
       const int total = min(S.samp_off[3] + S.nsamp[3], RCAP);
       if (tid == 0 && S.samp_off[3] + S.nsamp[3] > RCAP) atomicOr(b.status + f, kStatusQuadsOverflow);
       for (int t = tid; t < total; t += kDecodeThreads) {
@@ -3478,7 +3645,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
           gsy[t - kLdsRefine] = by;
         }
       }
-      __syncthreads();
+      team_sync<64>();
       phase(1);
       // per edge (lane e), the moments in the reference's sample order; samples are
       // staged 8 at a time in registers so their LDS reads overlap
@@ -3513,7 +3680,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
         S.lines[tid][2] = (double)det_cosf((float)nt);
         S.lines[tid][3] = (double)det_sinf((float)nt);
       }
-      __syncthreads();
+      team_sync<64>();
       phase(2);
       if (tid == 0) {
         float qp[4][2];
@@ -3536,7 +3703,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
         }
         for (int k = 0; k < 4; k++) { S.qc[k][0] = qp[k][0]; S.qc[k][1] = qp[k][1]; }
       }
-      __syncthreads();
+      team_sync<64>();
       phase(3);
     }
     if (prm.diag_stop == 6) continue;
@@ -3548,9 +3715,23 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
                           H[2] * (H[3] * H[7] - H[4] * H[6]);
       S.ok = hdet != 0;
     }
-    __syncthreads();
+    team_sync<64>();
     phase(4);
     if (!S.ok) continue;
+    uint32_t seq = 0;
+    if (POSE) {  // hand the homography and the unrotated corners to the pose wave
+      if (tid < 9) P.H[tid] = S.H[tid];
+      if (tid < 4) {
+        const int tcx = (tid == 1 || tid == 2) ? 1 : -1, tcy = tid < 2 ? 1 : -1;
+        hproject(S.H, tcx, tcy, &P.p[tid][0], &P.p[tid][1]);
+      }
+      seq = ++pose_seq;
+      team_sync<64>();
+      if (tid == 0) __hip_atomic_store(&P.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    uint32_t bc = 0xffffffffu;
+    double margin_d = -1;
+    do {
     // ---- quad_decode: border gray models (8 patterns x width_at_border <= 8
     // samples: lane = 8 * pattern + sample) ----
     const int wab = prm.fam.width_at_border, tw = prm.fam.total_width, nbits = prm.fam.nbits;
@@ -3571,7 +3752,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       S.gmv[tid] = S.gmvalid[tid] ? (double)gray[(size_t)iy * g.W + ix] : 0.0;
     }
     for (int t = tid; t < tw * tw; t += kDecodeThreads) S.values[t] = 0;
-    __syncthreads();
+    team_sync<64>();
     phase(5);
     // lane 0 builds and solves the white model, lane 1 the black one, each over
     // its 32 samples in the serial order, eight samples staged in registers at a time
@@ -3603,8 +3784,8 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       interp00 = gm_interp(m, 0, 0);
     }
     const double w00 = __shfl(interp00, 0), b00 = __shfl(interp00, 1);
-    __syncthreads();
-    if (w00 - b00 < 0) continue;  // uniform
+    team_sync<64>();
+    if (w00 - b00 < 0) break;  // uniform
     phase(6);
     if (tid < nbits) {
       const int bity = prm.fam.bity[tid], bitx = prm.fam.bitx[tid];
@@ -3624,7 +3805,7 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
         S.values[tw * (bity - minc) + bitx - minc] = v - (bth + wth) / 2.0;
       }
     }
-    __syncthreads();
+    team_sync<64>();
     phase(7);
     // sharpen (apriltag.c) over the total_width^2 grid: each lane owns cells t, t+64, t+128
     constexpr int kShR = (kMaxTotalWidth * kMaxTotalWidth + kDecodeThreads - 1) / kDecodeThreads;
@@ -3645,20 +3826,19 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
         shv[r] = acc;
       }
     }
-    __syncthreads();
+    team_sync<64>();
 #pragma unroll
     for (int r = 0; r < kShR; r++) {
       const int t = tid + 64 * r;
       if (t < tw * tw) S.values[t] = S.values[t] + prm.decode_sharpening * shv[r];
     }
-    __syncthreads();
+    team_sync<64>();
     // code word and scores: lane i reads bit i's value, the scores run in bit
     // order on every lane (uniform v_readlane loop), the word comes from a ballot
     double bitv = 0;
     if (tid < nbits) bitv = S.values[tw * (prm.fam.bity[tid] - minc) + prm.fam.bitx[tid] - minc];
     const uint64_t white_bits = __ballot(tid < nbits && bitv > 0);  // bit i: data bit i (MSB first in the word)
     const uint64_t rcode0 = __builtin_bitreverse64(white_bits) >> (64 - nbits);
-    double margin_d;
     {
       float black_score = 0, white_score = 0, black_cnt = 1, white_cnt = 1;
       for (int i = 0; i < nbits; i++) {
@@ -3671,7 +3851,6 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
     phase(8);
     // quick_decode_codeword: first rotation, then entry, within hamming <= 2
     // (codes are >= 5 apart, so at most one entry matches a rotation)
-    uint32_t bc = 0xffffffffu;
     {
       uint64_t r[4];
       r[0] = rcode0;
@@ -3687,6 +3866,11 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
       }
 #pragma unroll
       for (int d = 32; d > 0; d >>= 1) bc = min(bc, (uint32_t)__shfl_xor(bc, d));
+    }
+    } while (false);
+    if (POSE) {  // the pose of this quad is done before the next one is handed over
+      while (__hip_atomic_load(&P.ack, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq)
+        __builtin_amdgcn_s_sleep(1);
     }
     if (tid == 0) {
       const float margin = (float)margin_d;
@@ -3711,20 +3895,36 @@ __global__ __launch_bounds__(kDecodeThreads) __attribute__((amdgpu_waves_per_eu(
           hproject(d.H, tcx, tcy, &d.p[i][0], &d.p[i][1]);
         }
         d.frame = (uint16_t)f;
+        if (POSE) {
+          // R = R0 Rz(rot) with the exact quarter turn, t = t0
+          const int c = rot == 0 ? 1 : rot == 2 ? -1 : 0, sn = rot == 1 ? 1 : rot == 3 ? -1 : 0;
+          for (int i = 0; i < 3; i++) {
+            d.pose_R[i * 3 + 0] = P.R[i * 3 + 0] * c + P.R[i * 3 + 1] * sn;
+            d.pose_R[i * 3 + 1] = -P.R[i * 3 + 0] * sn + P.R[i * 3 + 1] * c;
+            d.pose_R[i * 3 + 2] = P.R[i * 3 + 2];
+          }
+          for (int k = 0; k < 3; k++) d.pose_t[k] = P.t[k];
+          d.pose_err[0] = P.err[0];
+          d.pose_err[1] = P.err[1];
+        }
         atomicAdd(b.ndets + f, 1u);
         const uint32_t di = atomicAdd(b.det_head, 1u);
         if (di < b.det_cap) {
           b.dets[di] = d;
-          b.hdets[di] = d;  // pose fields follow from k_pose
+          b.hdets[di] = d;  // (POSE: complete; else the pose fields follow from k_pose)
         }
         else atomicOr(b.status + f, kStatusDetsOverflow);
       }
     }
-    __syncthreads();
+    team_sync<64>();
     phase(9);
   }
   probe_flush(b, prm, pacc, 128, tid == 0);
   if (tid == 0) kt_end(b, 10);
+  if (POSE) {
+    if (tid == 0) __hip_atomic_store(&P.exit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    decode_finish(b, tid);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -4077,13 +4277,13 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     const bool cap4k = g.max_cluster <= 4096;
     if (!on(9)) return;
     if (g.ctw == 32 && cap4k) {  // latency mode: extents, SelectBlobs and keys in the blob team (no k_extents)
-      hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+      hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
     } else if (B < kWideBlobMaxBatch || prm.wide_blob) {
-      if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
-      else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+      hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
+      if (!cap4k) hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(512), 0, s, b, g, prm, 4096u);
     } else {
-      if (cap4k) hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm);
-      else hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(nblobwg), dim3(256), 0, s, b, g, prm);
+      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, 0u);
+      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(256), 0, s, b, g, prm, 4096u);
     }
     tk(9, s, 1);
   };
@@ -4111,12 +4311,17 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }
+  // latency mode: the pose inside k_decode (a second wave per workgroup) unless
+  // stages or one kernel are timed (the control block then leaves with k_pose,
+  // after the timed kernel's device-clock span)
+  const bool pose_fused = prm.tag_size > 0 && on(11) && B < kWideBlobMaxBatch && !ev && b.kt_stage < 0 && !kt;
   tk(10, st, 0);
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups
     // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
     const dim3 grd(decode_grid(nblobwg, B));
-    if (on(10)) hipLaunchKernelGGL(k_decode, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+    if (on(10) && pose_fused) hipLaunchKernelGGL(k_decode<true>, grd, dim3(128), 0, st, b, g, prm, B);
+    else if (on(10)) hipLaunchKernelGGL(k_decode<false>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
   }
   tk(10, st, 1);
   mark();
@@ -4126,7 +4331,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     hipLaunchKernelGGL(k_kt_span, dim3(1), dim3(256), 0, st, b);
   tk(11, st, 0);
   // latency mode: a wave per detection; throughput mode: four lanes per detection
-  if (prm.tag_size > 0 && on(11)) {
+  if (prm.tag_size > 0 && on(11) && !pose_fused) {
     if (B < kWideBlobMaxBatch) hipLaunchKernelGGL(k_pose<true>, dim3(32 * B), dim3(64), 0, st, b, prm);
     else hipLaunchKernelGGL(k_pose<false>, dim3(kPoseGroupsPerFrame * B), dim3(64), 0, st, b, prm);
   }

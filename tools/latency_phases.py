@@ -22,11 +22,17 @@ for rep in range(3):
 p = det.copy_probe().astype(np.int64)
 for name, base in (("k_blob_small", 64), ("k_blob", 80), ("k_decode", 128)):
     row = []
-    for k in range(1, 10):
+    for k in range(0, 10):
         t, n = p[base + k], p[base + 32 + k]
         if n:
             row.append("%d:%.2fus(x%d)" % (k, t / n / 100.0, n))
     print(name, " ".join(row))
+for name, idx in (("small", 200), ("large", 201)):
+    v = int(p[idx])
+    print("slowest %s item: %.2f us, %d points" % (name, (v >> 20) / 100.0, v & 0xfffff))
+nbig = max(1, int(p[220]))
+print("large blobs > 2048 points (%d): mean phase us" % int(p[220]), [round(p[208 + k] / 100.0 / nbig, 2) for k in range(10)])
+print("k_pairs phases (us): merge %.2f  list %.2f  rank %.2f  scan %.2f  work+bases %.2f" % tuple(np.diff(p[0:6]) / 100.0))
 print("pose phases (us): polar3 %.2f  OI-1 %.2f  ambiguity %.2f  OI-2 %.2f" % tuple(np.diff(p[16:21]) / 100.0))
 a = p[16 + 2]
 print("ambiguity detail (us): setup %.2f  deg2 %.2f  deg3 %.2f  deg4 %.2f  minima %.2f  rest %.2f" % (
