@@ -381,7 +381,6 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.par = (uint32_t*)dalloc(B * nd * 4);
   b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodesMax * 4);
   b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
-  b.blink = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 8 * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
   b.pts = (uint64_t*)dalloc(B * ntb * (size_t)g.bnd_region * 8);

@@ -197,7 +197,6 @@ struct DevBufs {
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
   uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodesMax] local roots of each CCL tile (global node ids)
   uint32_t* nlroot;   // [B][CTX*CTY]
-  uint32_t* blink;    // [B][CTX*CTY][8] k_thr_ccl's mask of the tile's border candidates that link
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile

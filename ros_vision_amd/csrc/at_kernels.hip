@@ -360,9 +360,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint32_t s_par[kCclTileNodes];
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
-  __shared__ uint32_t s_blink[8];  // this tile's k_ccl_border candidates that link (one bit per thread)
   if (tid == 0) s_nlr = 0;
-  if (tid < 8) s_blink[tid] = 0;
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
@@ -566,34 +564,6 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       hL = ((sr >> hl) & 1) ? slot_of<TWD>(bty, btx - (lane - hl), 2) : slot_of<TWD>(bty, btx - (lane - hl), 1);
     }
     hR = bg_in ? hL : R;
-    {
-      // k_ccl_border's link tests across the tile's top row / left and right columns
-      // (the reference's Merge conditions) on the threshold halo already in LDS: a
-      // bit per candidate, so that kernel reads one mask instead of the threshold plane
-      using BR = BorderRoles<TWD>;
-      const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
-      if (BY < g.BH && BX < g.BW && BY > 0 && bty == 0) {
-        const uint32_t m = (uint32_t)(a == 255 && T(pr - 1, pc - 1) == 255) |
-                           ((uint32_t)((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255)) << 1) |
-                           ((uint32_t)(bb == 255 && T(pr - 1, pc + 2) == 255) << 2) |
-                           ((uint32_t)(a == 0 && T(pr - 1, pc) == 0) << 3) | ((uint32_t)(bb == 0 && T(pr - 1, pc + 1) == 0) << 4);
-        for (int k = 0; k < 5; k++)
-          if ((m >> k) & 1) atomicOr(&s_blink[(btx * 5 + k) >> 5], 1u << ((btx * 5 + k) & 31));
-      }
-      if (BY < g.BH && BX < g.BW && BX > 0 && btx == 0) {
-        const uint32_t m = (uint32_t)(BY > 0 && bty > 0 && a == 255 && T(pr - 1, pc - 1) == 255) |
-                           ((uint32_t)((a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255)) << 1) |
-                           ((uint32_t)((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0)) << 2);
-        for (int k = 0; k < 3; k++) {
-          const int t = BR::Top + bty * 3 + k;
-          if ((m >> k) & 1) atomicOr(&s_blink[t >> 5], 1u << (t & 31));
-        }
-      }
-      if (BY < g.BH && BX < g.BW && BY > 0 && btx == kCclBW - 1 && bty >= 1 && bb == 255 && T(pr - 1, pc + 2) == 255) {
-        const int t = BR::Top + BR::Left + bty - 1;
-        atomicOr(&s_blink[t >> 5], 1u << (t & 31));
-      }
-    }
     s_par[F] = hF;
     s_par[L] = hL;
     s_par[R] = hR;
@@ -681,7 +651,6 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     if (cR && (wR & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
-  if (tid < 8) b.blink[((size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x) * 8 + tid] = s_blink[tid];
   if (tid == 0) {
     b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
     kt_end(b, 1);
@@ -763,26 +732,40 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
   }
   const int BY = blockIdx.y * kCclBH + bty, BX = blockIdx.x * kCclBW + btx;
   if (BY >= g.BH || BX >= g.BW) role = 3;
-  // which candidates link: k_thr_ccl's mask of this tile (one round trip, no
-  // threshold reads); the node pair of each candidate follows from its role
-  const uint32_t* bl = b.blink + ((size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x) * 8;
-  const bool link = role != 3 && ((bl[t >> 5] >> (t & 31)) & 1u);
+  const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
   const int Wd = g.Wd;
-  const uint32_t F = (uint32_t)((2 * BY) * Wd + 2 * BX), L = F + (uint32_t)Wd, R = L + 1;
-  uint32_t u = F, v = 0;
-  if (role == 0) {
-    if (kind == 0) v = F - 2 * Wd - 2;
-    else if (kind == 1) v = F - 2 * Wd;
-    else if (kind == 2) v = F - 2 * Wd + 2;
-    else if (kind == 3) { u = L; v = L - 2 * Wd; }
-    else { u = R; v = R - 2 * Wd; }
-  } else if (role == 1) {
-    if (kind == 0) v = F - 2 * Wd - 2;
-    else if (kind == 1) v = F - 2;
-    else { u = L; v = L - 1; }
-  } else {
-    v = F - 2 * Wd + 2;
+  const int row = 2 * BY, col = 2 * BX;
+  const size_t idx = (size_t)row * Wd + col;
+  auto px = [&](int r, int c) -> uint8_t {
+    if (r < 0 || c < 0 || r >= g.Hd || c >= g.Wd) return 127;
+    return thr[(size_t)r * Wd + c];
+  };
+  const bool act = role != 3;  // (no loads outside the image for the padding threads)
+  const uint8_t a = act ? thr[idx] : 127, bb = act ? thr[idx + 1] : 127, c = act ? thr[idx + Wd] : 127;
+  const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
+  uint32_t u = 0, v = 0;
+  bool link = false;
+  if (role == 0 && BY > 0) {
+    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255);
+      u = F; v = F - 2 * Wd;
+    }
+    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2; }
+    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - 2 * Wd; }
+    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - 2 * Wd; }
+  } else if (role == 1 && BX > 0) {
+    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    else if (kind == 1) {
+      link = (a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255);
+      u = F; v = F - 2;
+    } else {
+      link = (a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0);
+      u = L; v = L - 1;
+    }
+  } else if (role == 2 && BY > 0) {
+    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
   }
   if (link) g_union2(par, u, v);
   if (b.kt_stage == 2) {  // (uniform: the timed launch only)
@@ -1735,7 +1718,7 @@ __device__ int homography_wave(const float (*qc)[2], double* A, double* H) {
     else if (col == 8) v = cz;
     A[e] = v;
   }
-  __syncthreads();
+  team_sync<64>();  // (wave-level: k_decode<true> runs a second, independent wave)
   for (int col = 0; col < 8; col++) {
     // pivot: first row (col..7) holding the strict maximum of |A[row][col]| > 0
     double v = -1.0;
@@ -1760,14 +1743,14 @@ __device__ int homography_wave(const float (*qc)[2], double* A, double* H) {
       A[col * 9 + i] = A[row * 9 + i];
       A[row * 9 + i] = t;
     }
-    __syncthreads();
+    team_sync<64>();  // (wave-level: k_decode<true> runs a second, independent wave)
     const int nc = 8 - col;  // columns col+1..8
     if (lane < (7 - col) * nc) {
       const int i = col + 1 + lane / nc, j = col + 1 + lane % nc;
       const double fct = A[i * 9 + col] / A[col * 9 + col];
       A[i * 9 + j] -= fct * A[col * 9 + j];
     }
-    __syncthreads();
+    team_sync<64>();  // (wave-level: k_decode<true> runs a second, independent wave)
   }
   // back substitution, every lane in the serial order with the solution in
   // registers (the row's A reads are independent LDS broadcasts, issued together)
@@ -1783,7 +1766,7 @@ __device__ int homography_wave(const float (*qc)[2], double* A, double* H) {
   for (int k = 0; k < 8; k++)
     if (lane == k) H[k] = x[k];
   if (lane == 8) H[8] = 1;
-  __syncthreads();
+  team_sync<64>();  // (wave-level: k_decode<true> runs a second, independent wave)
   return 0;
 }
 
@@ -3471,12 +3454,16 @@ __device__ void pose_worker(PoseHandoff& P, const Params& prm) {
   }
 }
 // POSE: the last decode workgroup to finish copies the (final) control block to
-// the caller-visible host buffer (k_pose's job in the unfused sequence)
-__device__ void decode_finish(const DevBufs& b, int lane) {
-  uint32_t last = 0;
-  if (lane == 0) {
+// the caller-visible host buffer (k_pose's job in the unfused sequence).  Only the
+// min(grid, nq) workgroups that had a quad arrive (the others wrote nothing; one
+// arrival per workgroup on one counter costs ~12 ns each); no quad: workgroup 0.
+__device__ void decode_finish(const DevBufs& b, int lane, uint32_t nq) {
+  const uint32_t nwg = min(gridDim.x, nq);
+  if (blockIdx.x >= max(nwg, 1u)) return;
+  uint32_t last = nwg == 0;
+  if (lane == 0 && nwg) {
     __threadfence();
-    last = atomicAdd(b.dec_done, 1u) == gridDim.x - 1;
+    last = atomicAdd(b.dec_done, 1u) == nwg - 1;
   }
   last = __shfl(last, 0);
   if (!last) return;
@@ -3485,6 +3472,9 @@ __device__ void decode_finish(const DevBufs& b, int lane) {
     b.hctrl[w] = __hip_atomic_load(b.ctrl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef AT_POSE_IN_DECODE
+#define AT_POSE_IN_DECODE 1  // latency mode: the pose by a second wave of k_decode (0: k_pose)
+#endif
 #ifndef AT_DEC_WAVES
 #define AT_DEC_WAVES 2
 #endif
@@ -3923,7 +3913,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
   if (tid == 0) kt_end(b, 10);
   if (POSE) {
     if (tid == 0) __hip_atomic_store(&P.exit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    decode_finish(b, tid);
+    decode_finish(b, tid, nq);
   }
 }
 
@@ -4278,9 +4268,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     if (!on(9)) return;
     if (g.ctw == 32 && cap4k) {  // latency mode: extents, SelectBlobs and keys in the blob team (no k_extents)
       hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
-    } else if (B < kWideBlobMaxBatch || prm.wide_blob) {
-      hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
-      if (!cap4k) hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(512), 0, s, b, g, prm, 4096u);
+    } else if (B < kWideBlobMaxBatch || prm.wide_blob) {  // (latency: one launch, longest blob first)
+      if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
+      else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
     } else {
       hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, 0u);
       if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(256), 0, s, b, g, prm, 4096u);
@@ -4314,7 +4304,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   // latency mode: the pose inside k_decode (a second wave per workgroup) unless
   // stages or one kernel are timed (the control block then leaves with k_pose,
   // after the timed kernel's device-clock span)
-  const bool pose_fused = prm.tag_size > 0 && on(11) && B < kWideBlobMaxBatch && !ev && b.kt_stage < 0 && !kt;
+  const bool pose_fused = AT_POSE_IN_DECODE && prm.tag_size > 0 && on(11) && B < kWideBlobMaxBatch && !ev && b.kt_stage < 0 && !kt;
   tk(10, st, 0);
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups

@@ -18,6 +18,15 @@ if [ -n "${LAT_LIBS:-}" ]; then
   done
 fi
 if [ -n "${LIBS:-}" ]; then TAG=${TAG:-c2} bash tools/ab_stages.sh > /dev/null || exit 1; fi
+if [ -n "${LIBS1080:-}" ]; then
+  for r in 1 2; do for lib in $LIBS1080; do
+    echo -n "round=$r lib=$lib " >> $O/ab1080.txt
+    AT_HIP_LIB=$lib timeout -k 10 200 python bench.py --width 1920 --height 1080 --tags 24 --steps 40 --no-cpu-baseline --latency-frames 200 \
+      --host-ingest-steps 0 --c3-latency-iters 0 --no-kernel-timer 2>>$O/err.txt | python3 -c "
+import json,sys; j=json.load(sys.stdin); print(j['value'], j['p50_latency_hbm_ms'], j['detections_per_frame'], ' '.join('%s=%.4f' % kv for kv in j['stage_ms_per_batch'].items()))" >> $O/ab1080.txt || exit 1
+  done; done
+fi
+if [ -n "${PSTOPS:-}" ]; then TAG=${TAG:-c2}/abl STOPS=0 PSTOPS="$PSTOPS" bash tools/ablate.sh > /dev/null || exit 1; fi
 if [ -n "${EXTRA_LEGS:-}" ]; then
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --ingest scatter --no-cpu-baseline --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 > $O/bench_scatter_n1.json 2> $O/scatter.err || exit 1
   timeout -k 10 240 python bench.py --width 1920 --height 1080 --tags 24 --no-cpu-baseline --host-ingest-steps 0 --c3-latency-iters 0 > $O/bench_1080p.json 2> $O/bench_1080p.err || exit 1
