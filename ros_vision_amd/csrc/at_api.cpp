@@ -289,6 +289,10 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.BW = g.Wd / 2; g.BH = g.Hd / 2;
   g.ctw = d->B < kWideBlobMaxBatch ? 32 : 64;
   if (getenv("AT_CCL_TILE")) g.ctw = atoi(getenv("AT_CCL_TILE")) == 32 ? 32 : 64;
+  // size classes of the workgroup-team blob kernel (the rest: one wave per blob);
+  // latency mode gives the team blobs of more than 256 points too (its chain is
+  // the slowest single blob)
+  g.nlarge = (g.ctw == 32 && getenv("AT_NLARGE")) ? atoi(getenv("AT_NLARGE")) : kNumLargeCls;  // (experiment knob)
   g.CTX = (g.Wd + g.ctw - 1) / g.ctw;
   g.CTY = (g.Hd + kCclTileH - 1) / kCclTileH;
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);

@@ -114,6 +114,7 @@ struct Geom {
   int BW, BH;           // 2x2 CCL blocks
   int CTX, CTY;         // CCL tiles
   int ctw;              // CCL tile width (32: latency mode, 64: throughput mode)
+  int nlarge;           // size classes 0 .. nlarge-1 go to the workgroup-team blob kernel
   int bnd_region;       // points per k_boundary tile region (kBndPts)
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)
   int BTX, BTY, ntb;    // k_boundary tiles (64 x 4*kBndRows interior pixels each)

@@ -3207,7 +3207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVE
   for (int c = 0; c < kNumCls; c++) {
     cnt[c] = min(b.ncls[c], b.wcap);
     total += cnt[c];
-    if (c < kNumLargeCls) nlarge += cnt[c];
+    if (c < g.nlarge) nlarge += cnt[c];
   }
   for (uint32_t it = blockIdx.x; it < nlarge; it += gridDim.x) {
     uint32_t w = 0;
@@ -3268,7 +3268,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
   load_combos(s_combo, tid, NT);
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
   __syncthreads();
-  const int ncls = nlo ? 1 : kNumLargeCls;  // (blobs over 4096 points are all in class 0)
+  const int ncls = nlo ? 1 : g.nlarge;  // (blobs over 4096 points are all in class 0)
   uint32_t nwork = 0;
   for (int c = 0; c < ncls; c++) nwork += s_cnt[c];
   uint32_t* head = nlo ? b.workhead_small : b.workhead;
@@ -3315,7 +3315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
   __syncthreads();
   uint32_t nwork = 0;
-  for (int c = kNumLargeCls; c < kNumCls; c++) nwork += s_cnt[c];
+  for (int c = g.nlarge; c < kNumCls; c++) nwork += s_cnt[c];
   // static round-robin over the size-ordered list: no dequeue atomic (a
   // device-scope atomic on one hot address is serviced at the memory side; one
   // per small blob serialized every wave of the chip behind that address)
@@ -3326,15 +3326,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
   uint32_t w = 0, w1 = 0;
   PairInfo pi = {0, 0, 0};
   if (item < nwork) {
-    work_item(b, s_cnt, kNumLargeCls, kNumCls, item, &w);
+    work_item(b, s_cnt, g.nlarge, kNumCls, item, &w);
     pi = load_pair_info(b, w);
   }
-  if (item + nwaves < nwork) work_item(b, s_cnt, kNumLargeCls, kNumCls, item + nwaves, &w1);
+  if (item + nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + nwaves, &w1);
   for (; item < nwork; item += nwaves) {
     const bool has1 = item + nwaves < nwork;
     const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
     uint32_t w2 = 0;
-    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, kNumLargeCls, kNumCls, item + 2 * nwaves, &w2);
+    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + 2 * nwaves, &w2);
     blob_item<64, kSmallBlob, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
     w = w1;
     pi = pi1;

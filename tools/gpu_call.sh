@@ -17,6 +17,20 @@ if [ -n "${LAT_LIBS:-}" ]; then
     AT_HIP_LIB=$lib timeout -k 10 120 python tools/latency_phases.py 1 >> $O/lat.txt 2>&1 || exit 1
   done
 fi
+if [ -n "${LAT_ENVS:-}" ]; then
+  for r in 1 2; do for ev in $LAT_ENVS; do
+    echo "== $ev" >> $O/lat_env.txt
+    env $ev timeout -k 10 120 python tools/lat_stages.py 300 2>&1 | grep wall >> $O/lat_env.txt || exit 1
+  done; done
+fi
+if [ -n "${C3_ENVS:-}" ]; then
+  for r in 1 2; do for ev in $C3_ENVS; do
+    echo -n "round=$r $ev " >> $O/c3_env.txt
+    env $ev timeout -k 10 200 python bench.py --steps 10 --no-cpu-baseline --no-stage-profile --host-ingest-steps 0 --latency-frames 500 \
+      2>>$O/err.txt | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['p50_latency_ms'], j['p50_latency_hbm_ms'], j['p50_latency_c3_ms'])" >> $O/c3_env.txt || exit 1
+  done; done
+fi
+if [ -n "${PROFILE:-}" ]; then bash tools/profile_round.sh $PROFILE > /dev/null || exit 1; fi
 if [ -n "${LIBS:-}" ]; then TAG=${TAG:-c2} bash tools/ab_stages.sh > /dev/null || exit 1; fi
 if [ -n "${LIBS1080:-}" ]; then
   for r in 1 2; do for lib in $LIBS1080; do
