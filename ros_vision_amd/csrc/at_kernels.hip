@@ -2780,6 +2780,21 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     const int ntop = npk < (uint32_t)kNMaxima ? (int)npk : kNMaxima;
     uint64_t last = 0;
     if constexpr (NT == 64) {
+      if (npk <= 64) {  // (uniform) the usual blob: the peaks compacted in LDS, each lane ranks one
+        uint64_t* pall = reinterpret_cast<uint64_t*>(errv);  // (errv is dead: staged in ew)
+        team_sync<64>();
+        uint32_t pos = wave_incl_scan(nmine, AddOp(), 0u) - nmine;
+#pragma unroll
+        for (int j = 0; j < kPR; j++)
+          if (mine[j] != ~0ull) pall[pos++] = mine[j];
+        team_sync<64>();
+        if (lane < npk) {
+          const uint64_t pv = pall[lane];
+          uint32_t r = 0;
+          for (uint32_t j = 0; j < npk; j++) r += pall[j] < pv;  // (broadcast reads)
+          if (r < (uint32_t)kNMaxima) pks[r] = pv;
+        }
+      } else {
       for (int r = 0; r < ntop; r++) {
         uint64_t m = ~0ull;
 #pragma unroll
@@ -2790,6 +2805,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
         m = wave_reduce(m, MinOp());
         if (tid == 0) pks[r] = m;
         last = m;
+      }
       }
     } else {
       // every wave selects its own top ntop (wave minima, no barriers), then wave 0

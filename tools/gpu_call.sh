@@ -31,6 +31,12 @@ if [ -n "${C3_ENVS:-}" ]; then
   done; done
 fi
 if [ -n "${PROFILE:-}" ]; then bash tools/profile_round.sh $PROFILE > /dev/null || exit 1; fi
+if [ -n "${PHASE_LIBS:-}" ]; then
+  for lib in $PHASE_LIBS; do
+    echo "== $lib B=${PHASE_B:-128}" >> $O/phases.txt
+    AT_HIP_LIB=$lib timeout -k 10 120 python tools/latency_phases.py ${PHASE_B:-128} 2>&1 | grep -v amdgpu >> $O/phases.txt || exit 1
+  done
+fi
 if [ -n "${LIBS:-}" ]; then TAG=${TAG:-c2} bash tools/ab_stages.sh > /dev/null || exit 1; fi
 if [ -n "${LIBS1080:-}" ]; then
   for r in 1 2; do for lib in $LIBS1080; do
