@@ -268,7 +268,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (!cfg || !cam || !out) return AT_E_INVALID;
   *out = nullptr;
   const FamilyInfo* fam = find_family(cfg->family);
-  if (!fam) return AT_E_FAMILY;
+  if (!fam || fam->ncodes > kMaxCodes) return AT_E_FAMILY;
   const int W = cfg->width, H = cfg->height;
   // GpuDetector preconditions (apriltag_gpu.cu:166-167, 754-755, 774; line_fit_filter.cu:1205)
   if (W <= 16 || H <= 16 || W % 8 || H % 8 || (long)W * H >= (1L << 22)) return AT_E_INVALID;
