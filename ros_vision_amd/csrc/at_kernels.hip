@@ -1138,7 +1138,10 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   stamp(0);
   __shared__ uint64_t t_key[kHashSlots];
   __shared__ uint32_t t_cnt[kHashSlots];
-  __shared__ uint64_t s_list[kMaxPairs];
+  // the frame's pair list, sorted, lives in t_key's storage once the lookup table
+  // is out (54 KB of LDS instead of 86 KB: the batches in flight co-reside better)
+  uint64_t* s_list = t_key;
+  static_assert(kMaxPairs <= kHashSlots, "the pair list fits in the hash table's storage");
   __shared__ uint32_t s_n, s_full, s_np;
   __shared__ uint32_t s_wsum[16];
   for (int i = tid; i < kHashSlots; i += 1024) {
@@ -1274,11 +1277,23 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   }
   __syncthreads();
   stamp(1);
-  for (int s = tid; s < kHashSlots; s += 1024) {
-    const uint64_t k = t_key[s];
-    if (k) {
+  // the lookup table used by k_group (keys of every slot, 0 = empty), then the
+  // occupied slots listed over t_key's storage
+  static_assert(kHashSlots == 4 * 1024, "four hash slots per thread");
+  uint64_t kreg[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int s = tid + 1024 * k;
+    kreg[k] = t_key[s];
+    b.ht_key[(size_t)f * kHashSlots + s] = kreg[k];
+    b.ht_cnt[(size_t)f * kHashSlots + s] = t_cnt[s];
+  }
+  __syncthreads();  // every t_key read before the list overwrites it
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (kreg[k]) {
       const uint32_t i = atomicAdd(&s_n, 1u);
-      if (i < kMaxPairs) s_list[i] = (k << kHashBits) | (uint64_t)s;
+      if (i < kMaxPairs) s_list[i] = (kreg[k] << kHashBits) | (uint64_t)(tid + 1024 * k);
     }
   }
   __syncthreads();
@@ -1288,21 +1303,16 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
     if (tid == 0) atomicOr(b.status + f, s_full ? kStatusHashFull : kStatusPairsOverflow);
     return;
   }
-  // the lookup table used by k_group: keys of every slot (0 = empty)
-  for (int s = tid; s < kHashSlots; s += 1024) {
-    b.ht_key[(size_t)f * kHashSlots + s] = t_key[s];
-    b.ht_cnt[(size_t)f * kHashSlots + s] = t_cnt[s];
-  }
   int np2 = 64;
   while (np2 < (int)n) np2 <<= 1;
   for (int i = (int)n + tid; i < np2; i += 1024) s_list[i] = ~0ull;
   __syncthreads();
   stamp(2);
   if (n <= 1024) {
-    // rank sort (keys are unique: the slot rides in the low bits); t_key is free
-    // once the lookup table has been written out above.  P = 1024 / n threads per
-    // key, each counting the smaller keys of a 1/P slice of the list (a frame's
-    // ~400 pairs: 2 threads per key, half the serial LDS reads)
+    // rank sort (keys are unique: the slot rides in the low bits), the list in
+    // t_key[0, n), the ranked copy in t_key[1024, 1024 + n), the ranks after it.
+    // P = 1024 / n threads per key, each counting the smaller keys of a 1/P slice
+    // of the list (a frame's ~400 pairs: 2 threads per key, half the serial LDS reads)
     const int P = (int)(1024 / (n ? n : 1u));
     uint32_t* s_rank = reinterpret_cast<uint32_t*>(t_key + 2048);
     if (tid < (int)n) s_rank[tid] = 0;
@@ -1319,19 +1329,23 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
       if (r) atomicAdd(&s_rank[i], r);
     }
     __syncthreads();
-    if (tid < (int)n) t_key[s_rank[tid]] = s_list[tid];
+    if (tid < (int)n) t_key[1024 + s_rank[tid]] = s_list[tid];
     __syncthreads();
-    if (tid < (int)n) s_list[tid] = t_key[tid];
+    if (tid < (int)n) s_list[tid] = t_key[1024 + tid];
     __syncthreads();
   } else {
     block_bitonic_sort<uint64_t, 1024>(s_list, np2);
   }
   stamp(3);
   // counts in rank order (straight from the hash slots), exclusive scan -> offsets;
-  // each thread owns 4 consecutive ranks
+  // each thread owns 4 consecutive ranks, whose hash slots it keeps in registers
+  // (t_key's storage is reused for the segment cursors below)
   const int i0 = tid * 4;
-  auto cnt_at = [&](int i) -> uint32_t { return i < (int)n ? t_cnt[s_list[i] & (kHashSlots - 1)] : 0u; };
-  const uint32_t c0 = cnt_at(i0), c1 = cnt_at(i0 + 1), c2 = cnt_at(i0 + 2), c3 = cnt_at(i0 + 3);
+  uint32_t lslt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) lslt[k] = i0 + k < (int)n ? (uint32_t)(s_list[i0 + k] & (kHashSlots - 1)) : 0u;
+  auto cnt_at = [&](int k) -> uint32_t { return i0 + k < (int)n ? t_cnt[lslt[k]] : 0u; };
+  const uint32_t c0 = cnt_at(0), c1 = cnt_at(1), c2 = cnt_at(2), c3 = cnt_at(3);
   const uint32_t tsum = c0 + c1 + c2 + c3;
   const uint32_t incl = wave_incl_scan(tsum, AddOp(), 0u);
   const uint32_t lane = lane_id();
@@ -1367,7 +1381,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
     if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      const uint32_t slot = lslt[k];
       b.ht_rank[(size_t)f * kHashSlots + slot] = (uint32_t)i;
       b.ht_off[(size_t)f * kHashSlots + slot] = offs[k];
       b.pair_cnt[(size_t)f * kMaxPairs + i] = cs[k];
@@ -1386,7 +1400,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
     if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      const uint32_t slot = lslt[k];
       t_off[slot] = offs[k];
       t_cur[slot] = 0;
     }
@@ -1407,7 +1421,7 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   for (int k = 0; k < 4; k++) {
     const int i = i0 + k;
     if (i < (int)n) {
-      const uint32_t slot = (uint32_t)(s_list[i] & (kHashSlots - 1));
+      const uint32_t slot = lslt[k];
       b.ht_cur[(size_t)f * kHashSlots + slot] = t_cur[slot];
     }
   }
