@@ -3501,6 +3501,9 @@ __device__ void decode_finish(const DevBufs& b, int lane, uint32_t nq) {
     b.hctrl[w] = __hip_atomic_load(b.ctrl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef AT_FORK_SMALL
+#define AT_FORK_SMALL 1  // latency mode: fork the small-blob kernel (0: the large-blob one)
+#endif
 #ifndef AT_POSE_IN_DECODE
 #define AT_POSE_IN_DECODE 1  // latency mode: the pose by a second wave of k_decode (0: k_pose)
 #endif
@@ -4322,11 +4325,17 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     hipError_t e;
     if ((e = hipEventRecord(fork, st))) return e;
     if ((e = hipStreamWaitEvent(st2, fork, 0))) return e;
-    // the small-blob kernel stays on the main stream (no cross-queue wait before
-    // it); the large-blob kernel, which finishes first, is the forked one, so the
-    // join's wait is on a signal that has usually fired: ~5 us less at B = 1
-    blob_small(st);
-    blob_large(st2);
+    // the kernel that finishes last stays on the main stream, so neither the fork's
+    // start delay nor the join's wait lies on the chain: the large-blob kernel
+    // (extents, keys and up to 4096 points per team: ~43 us at B = 1) on the main
+    // stream, the small-blob kernel (~35 us) forked
+    if (AT_FORK_SMALL) {
+      blob_large(st);
+      blob_small(st2);
+    } else {
+      blob_small(st);
+      blob_large(st2);
+    }
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
   }

@@ -12,7 +12,7 @@ ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
              r["Kernel_Name"].split("(")[0].replace("void ", "").replace("at::", "")) for r in rows)
 chains, cur = [], []
 for s, e, n in ev:
-    if n.startswith("k_pre") and cur:
+    if (n.startswith("k_pre") or n.startswith("k_thr_ccl")) and cur and not cur[-1][2].startswith("k_pre"):
         chains.append(cur)
         cur = []
     cur.append((s, e, n))

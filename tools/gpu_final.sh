@@ -1,0 +1,10 @@
+# End-of-session evidence in one GPU call: GPU tests + smoke of the tree, the B=1
+# kernel chain (rocprofv3 kernel trace of tools/lat_trace.py), the full profile set
+# (tools/profile_round.sh) and the default bench line.  usage: bash tools/gpu_final.sh TAG
+set -o pipefail
+TAG=${1:-final}; O=gpurun_out/$TAG; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/lat_trace -o run -- python3 $GRAFT_REPO_ROOT/tools/lat_trace.py 300 > /dev/null 2>&1) || exit 1
+python3 tools/gap_report.py $O/lat_trace/run_kernel_trace.csv > $O/lat_gaps.txt || exit 1
+bash tools/profile_round.sh $TAG > /dev/null || exit 1
