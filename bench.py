@@ -191,7 +191,6 @@ def main():
     from ros_vision_amd import multigpu
     from ros_vision_amd.stream import StreamRunner
     W, H, B = args.width, args.height, args.batch
-    assert args.pool % B == 0 or B % args.pool == 0 or args.pool >= B
     scatter = args.ingest == "scatter"
     frames = render_pool(args, rank)
     # scatter: rank 0's pool per rank holds at least one batch (the pool repeated)
@@ -200,6 +199,7 @@ def main():
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
     npool = args.pool * copies
+    assert npool >= B, "the frames resident per GPU (--pool x --hbm-copies) must hold one batch"
     dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank, pinned_out=scatter) for _ in range(args.instances)]
     ingest = None
     if scatter:

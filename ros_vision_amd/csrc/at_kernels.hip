@@ -1207,17 +1207,37 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
   auto merge_pass = [&](uint64_t limit) {
 #pragma unroll
     for (int k = 0; k < kPairsEntCache; k++) { c_slot[k] = 0xffffffffu; c_cnt[k] = 0; c_idx[k] = 0; c_lds[k] = false; }
-    for (uint32_t i = tid, k = 0; i < tot_e; i += 1024, k++) {
+    {
+      // the thread's first kPairsEntCache entries: every index first, then every
+      // load, then the merges (one global round trip for all of them)
+      uint32_t et[kPairsEntCache], cnt[kPairsEntCache];
+      uint64_t key[kPairsEntCache];
+      size_t e[kPairsEntCache];
+#pragma unroll
+      for (int k = 0; k < kPairsEntCache; k++) {
+        const uint32_t i = tid + 1024u * k;
+        e[k] = i < tot_e ? entry(i, &et[k]) : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPairsEntCache; k++) {
+        const bool in = tid + 1024u * k < tot_e;
+        cnt[k] = in ? b.pent_cnt[e[k]] : 0u;
+        key[k] = in ? b.pent_key[e[k]] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kPairsEntCache; k++) {
+        if (tid + 1024u * k >= tot_e) continue;
+        c_slot[k] = key[k] < limit ? merge(key[k], cnt[k]) : 0xffffffffu;
+        c_cnt[k] = cnt[k];
+        c_idx[k] = (uint32_t)e[k];
+        c_lds[k] = et[k] < (uint32_t)kGrpEnt;
+      }
+    }
+    for (uint32_t i = tid + 1024u * kPairsEntCache; i < tot_e; i += 1024) {  // (crowded frames)
       uint32_t et;
       const size_t e = entry(i, &et);
-      const uint32_t cnt = b.pent_cnt[e];
       const uint64_t key = b.pent_key[e];
-      const uint32_t slot = key < limit ? merge(key, cnt) : 0xffffffffu;
-      if (k < (uint32_t)kPairsEntCache) {
-#pragma unroll
-        for (int kk = 0; kk < kPairsEntCache; kk++)  // (constant register indices)
-          if (kk == (int)k) { c_slot[kk] = slot; c_cnt[kk] = cnt; c_idx[kk] = (uint32_t)e; c_lds[kk] = et < (uint32_t)kGrpEnt; }
-      }
+      if (key < limit) merge(key, b.pent_cnt[e]);
     }
     for (uint32_t i = tid; i < novf; i += 1024) {
       const uint64_t key = b.povf_key[(size_t)f * kPairEntCap + i];

@@ -9,7 +9,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     for cfg in "${LIST[@]}"; do
       read -r inst batch <<< "$cfg"
       echo -n "round=$r K=$k inst=$inst batch=$batch " >> $OUT/r.txt
-      timeout -k 10 150 python3 bench.py --instances $inst --batch $batch --pool 192 --hw-queues ${HWQ:-8} --steps $k --warmup 5 --no-cpu-baseline \
+      timeout -k 10 150 python3 bench.py --instances $inst --batch $batch --pool ${POOL:-64} --hw-queues ${HWQ:-8} --steps $k --warmup 5 --no-cpu-baseline \
         --latency-frames 0 --no-stage-profile --timed-kernel k_blob_small 2>>$OUT/err.txt \
         | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['value'], j['ms_per_step'])" >> $OUT/r.txt || exit 1
     done
