@@ -83,7 +83,8 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_pre":
         return nf * (2 * W * H + W * H + Wd * Hd)           # YUYV in, gray + decimated out
     if kernel == "k_boundary":
-        return nf * 5 * Wd * Hd + 8 * stats.get("boundary_points", 0)  # thr + labels in, points out
+        # thr + labels in; points out as the 4-B (pair entry, point bits) words of narrow tiles
+        return nf * 5 * Wd * Hd + 4 * stats.get("boundary_points", 0)
     if kernel == "k_blob":  # kept blobs: the 8-B sort key of every point (the line-fit weight W rides in it)
         return 8 * stats.get("large_blob_points", 0)
     if kernel == "k_blob_small":
