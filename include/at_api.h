@@ -140,7 +140,10 @@ enum {
   AT_STAGE_PROBE = 11       /* u64[256] kernel phase clock stamps when AT_PHASE_PROBE is set (diagnostic) */
 };
 long long at_debug_copy(at_detector *d, int stage, int frame, void *dst, size_t bytes);
-/* AT_STAGE_BLOB_POINTS needs the blob kernels to write the sorted IndexPoint keys
+/* AT_STAGE_GRAY: the full-resolution gray plane is written for BGR8 batches (k_decode
+ * samples it) and, for YUYV / GRAY8 batches, only while the debug taps are on (k_decode
+ * then reads the frame's own luma); AT_E_INVALID otherwise.
+ * AT_STAGE_BLOB_POINTS needs the blob kernels to write the sorted IndexPoint keys
  * back (8 B per point of every selected blob): off by default (production), on
  * with at_set_debug_taps(d, 1) for parity checks; AT_E_INVALID while off. */
 int at_set_debug_taps(at_detector *d, int enable);

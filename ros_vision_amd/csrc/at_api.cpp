@@ -146,6 +146,7 @@ struct at_detector {
   std::vector<int> res_idx, res_off, res_n;
   int last_nframes;
   int last_fmt;
+  int last_gray;            // the last batch wrote the gray plane (AT_STAGE_GRAY)
   int last_staged;          // the last batch's frames were host frames staged in d_in (at_detect*)
   int last_gp;              // the last batch ran the game-piece preprocessing (k_gp_pre)
   int pending;
@@ -322,6 +323,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.taps = 0;  // debug taps off: at_set_debug_taps
   p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
   p.pipe_stop = getenv("AT_DIAG_PIPE_STOP") ? atoi(getenv("AT_DIAG_PIPE_STOP")) : 0;
+  p.lblob_wg = getenv("AT_LBLOB_WG") ? std::max(16, atoi(getenv("AT_LBLOB_WG"))) : 0;  // experiment
+  p.sblob_wg = getenv("AT_SBLOB_WG") ? std::max(16, atoi(getenv("AT_SBLOB_WG"))) : 0;  // experiment
   p.fam = family_desc(*fam);
   d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {
@@ -673,6 +676,7 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   HIPCHK(hipEventRecord(d->ev_done, st));
   d->last_nframes = nframes;
   d->last_fmt = fmt;
+  d->last_gray = fmt == AT_FMT_BGR8 || d->prm.taps;  // (YUYV / GRAY8: k_decode samples the frame)
   d->last_gp = d->prm.gp_c && fmt == AT_FMT_BGR8;
   d->pending = 1;
   return AT_OK;
@@ -1122,7 +1126,9 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
   const int B = d->B;
   std::vector<uint8_t> tmp;
   switch (stage) {
-    case AT_STAGE_GRAY: src = d->d.gray + frame * npix; n = npix; break;
+    case AT_STAGE_GRAY:
+      if (!d->last_gray) return AT_E_INVALID;  // YUYV / GRAY8 batches without the debug taps
+      src = d->d.gray + frame * npix; n = npix; break;
     case AT_STAGE_DECIMATED: src = d->d.dec + frame * nd; n = nd; break;
     case AT_STAGE_THRESHOLD: src = d->d.thr + frame * nd; n = nd; break;
     case AT_STAGE_LABELS: {

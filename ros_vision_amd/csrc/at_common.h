@@ -136,6 +136,8 @@ struct Params {
   int taps;       // write the sorted IndexPoint parity tap (AT_STAGE_BLOB_POINTS) over the grouped points
   int wide_blob;  // AT_WIDE_BLOB=1: 512-thread large-blob teams at every batch size (experiment)
   int pipe_stop;  // diagnostics only (AT_DIAG_PIPE_STOP): launch the stages < N only; 0 = all
+  int lblob_wg;   // throughput-mode large-blob kernel's persistent grid (AT_LBLOB_WG; 0: nblobwg)
+  int sblob_wg;   // small-blob kernel's persistent grid (AT_SBLOB_WG; 0: 2 nblobwg)
   FamilyDesc fam;
   int gp_w, gp_h, gp_c;  // game-piece preprocessing output (at_gp_enable); gp_c == 0: off
 };

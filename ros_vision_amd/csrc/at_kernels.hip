@@ -229,8 +229,11 @@ __device__ __forceinline__ void load_y8(const uint8_t* in, int W, int row, int x
   }
 }
 
+// wgray: write the full-resolution gray plane (BGR8 input, whose luma k_decode
+// samples from it, or the parity taps); YUYV / GRAY8 frames carry their luma
+// already, so k_decode samples the frame and the plane is not written
 template <int FMT>
-__global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
+__global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g, int wgray) {
   const int f = blockIdx.z;
   const int tx = blockIdx.x * 64 + threadIdx.x;
   const int ty = blockIdx.y * 4 + threadIdx.y;
@@ -249,10 +252,12 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g) {
     const int row = ty * 8 + r;
     uint32_t y[8];
     load_y8<FMT>(in, g.W, row, x0, y);
-    uint2 gw;
-    gw.x = y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24);
-    gw.y = y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24);
-    *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x0) = gw;
+    if (FMT == 1 || wgray) {
+      uint2 gw;
+      gw.x = y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24);
+      gw.y = y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24);
+      *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x0) = gw;
+    }
     if ((r & 1) == 0) {
       const uint32_t d = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
       *reinterpret_cast<uint32_t*>(dec + (size_t)(row >> 1) * g.Wd + (x0 >> 1)) = d;
@@ -414,8 +419,9 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       const int lr = i / kCR, row = 2 * y0 + lr, x = 2 * x0 + 8 * (i % kCR);
       if (i < 2 * kCclTileH * kCR && row < g.H && x < g.W) {
         const uint32_t(&y)[8] = yin[k];
-        *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x) =
-            make_uint2(y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24), y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24));
+        if (PRE == 1 || prm.taps)  // (k_decode samples YUYV / GRAY8 frames directly)
+          *reinterpret_cast<uint2*>(gray + (size_t)row * g.W + x) =
+              make_uint2(y[0] | (y[1] << 8) | (y[2] << 16) | (y[3] << 24), y[4] | (y[5] << 8) | (y[6] << 16) | (y[7] << 24));
         if ((lr & 1) == 0) {
           const uint32_t d = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
           *reinterpret_cast<uint32_t*>(decw + (size_t)(row >> 1) * g.Wd + (x >> 1)) = d;
@@ -3538,7 +3544,7 @@ __device__ void decode_finish(const DevBufs& b, int lane, uint32_t nq) {
 // the tag frame), so the B = 1 chain is homography + pose instead of decode +
 // pose.  The last workgroup to finish hands the control block to the host.
 template <bool POSE>
-__global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_waves_per_eu(POSE ? 1 : AT_DEC_WAVES))) void k_decode(DevBufs b, Geom g, Params prm, int B) {
+__global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_waves_per_eu(POSE ? 1 : AT_DEC_WAVES))) void k_decode(DevBufs b, Geom g, Params prm, int B, int fmt) {
   constexpr int RCAP = kMaxRefineSamples;
   __shared__ DecodeShared S;
   __shared__ PoseHandoff P;
@@ -3605,7 +3611,11 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
     const QuadCand& qd = b.qcand[(size_t)lo * kQuadCandPerFrame + (item - qpre[lo])];
     const int f = (int)qd.frame;
     const uint32_t qrank = qd.rank;
-    const uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
+    // luma of pixel i = y W + x: the frame's own Y bytes for YUYV (every second byte)
+    // and GRAY8 input, the gray plane k_pre wrote for BGR8
+    const uint8_t* gsrc = fmt == 1 ? b.gray + (size_t)f * g.W * g.H : b.frames[f];
+    const int gsh = fmt == 0 ? 1 : 0;
+    auto pix = [&](size_t i) -> uint32_t { return gsrc[i << gsh]; };
     if (tid < 4) { S.qc[tid][0] = qd.p[tid][0]; S.qc[tid][1] = qd.p[tid][1]; }
     team_sync<64>();
     phase(0);
@@ -3655,8 +3665,8 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
           g1v[k] = -1;
           g2v[k] = 0;
           if (in) {
-            g1v[k] = gray[y1 * g.W + x1];
-            g2v[k] = gray[y2 * g.W + x2];
+            g1v[k] = (int)pix((size_t)y1 * g.W + x1);
+            g2v[k] = (int)pix((size_t)y2 * g.W + x2);
           }
         }
         double Mn = 0, Mcount = 0;
@@ -3788,7 +3798,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
       S.gmx[tid] = tagx;
       S.gmy[tid] = tagy;
       S.gmvalid[tid] = i < wab && !(ix < 0 || iy < 0 || ix >= g.W || iy >= g.H);
-      S.gmv[tid] = S.gmvalid[tid] ? (double)gray[(size_t)iy * g.W + ix] : 0.0;
+      S.gmv[tid] = S.gmvalid[tid] ? (double)pix((size_t)iy * g.W + ix) : 0.0;
     }
     for (int t = tid; t < tw * tw; t += kDecodeThreads) S.values[t] = 0;
     team_sync<64>();
@@ -3837,8 +3847,8 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
       const int y1 = (int)floor(py - 0.5), y2 = (int)ceil(py - 0.5);
       const double yy = py - 0.5 - y1;
       if (!(x1 < 0 || x2 >= g.W || y1 < 0 || y2 >= g.H)) {  // value_for_pixel
-        const double v = gray[(size_t)y1 * g.W + x1] * (1 - xx) * (1 - yy) + gray[(size_t)y1 * g.W + x2] * xx * (1 - yy) +
-                         gray[(size_t)y2 * g.W + x1] * (1 - xx) * yy + gray[(size_t)y2 * g.W + x2] * xx * yy;
+        const double v = (int)pix((size_t)y1 * g.W + x1) * (1 - xx) * (1 - yy) + (int)pix((size_t)y1 * g.W + x2) * xx * (1 - yy) +
+                         (int)pix((size_t)y2 * g.W + x1) * (1 - xx) * yy + (int)pix((size_t)y2 * g.W + x2) * xx * yy;
         const double bth = S.bC[0] * tagx + S.bC[1] * tagy + S.bC[2];
         const double wth = S.wC[0] * tagx + S.wC[1] * tagy + S.wC[2];
         S.values[tw * (bity - minc) + bitx - minc] = v - (bth + wth) / 2.0;
@@ -4253,9 +4263,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     // latency mode: k_thr_ccl does k_pre's work (one launch less on the B = 1 chain;
     // in throughput mode the longer k_thr_ccl costs ~6 % of concurrent throughput)
     if (!on(0) || g.ctw == 32) {}
-    else if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g);
-    else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g);
-    else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g);
+    else if (fmt == 0) hipLaunchKernelGGL(k_pre<0>, grd, blk, 0, st, b, g, prm.taps);
+    else if (fmt == 1) hipLaunchKernelGGL(k_pre<1>, grd, blk, 0, st, b, g, 1);
+    else hipLaunchKernelGGL(k_pre<2>, grd, blk, 0, st, b, g, prm.taps);
     tk(0, st, 1);
     // game-piece network input from the same BGR frames (counted in stage 0's time)
     if (on(0) && prm.gp_c && fmt == 1)
@@ -4324,7 +4334,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
     } else {
-      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, 0u);
+      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u);
       if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(256), 0, s, b, g, prm, 4096u);
     }
     tk(9, s, 1);
@@ -4333,7 +4343,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(8, s, 0);
     if (!on(8)) {}
     else if (fuse_small) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
-    else hipLaunchKernelGGL(k_blob_small<false>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    else hipLaunchKernelGGL(k_blob_small<false>, dim3(prm.sblob_wg ? prm.sblob_wg : nblobwg * 2), dim3(256), 0, s, b, g, prm);
     tk(8, s, 1);
   };
   if (ev || !st2) {
@@ -4368,8 +4378,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     // one wave per workgroup, persistent over the accepted quads: enough groups
     // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
     const dim3 grd(decode_grid(nblobwg, B));
-    if (on(10) && pose_fused) hipLaunchKernelGGL(k_decode<true>, grd, dim3(128), 0, st, b, g, prm, B);
-    else if (on(10)) hipLaunchKernelGGL(k_decode<false>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B);
+    if (on(10) && pose_fused) hipLaunchKernelGGL(k_decode<true>, grd, dim3(128), 0, st, b, g, prm, B, fmt);
+    else if (on(10)) hipLaunchKernelGGL(k_decode<false>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B, fmt);
   }
   tk(10, st, 1);
   mark();
