@@ -19,8 +19,15 @@ export TMPDIR=/tmp
 ONLY="--latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0"
 SHORT="$ROOT/bench.py --no-cpu-baseline --no-stage-profile --batch $BATCH --steps 4 --warmup 1 $ONLY"
 cd /tmp
+# the traced run times the kernel the bench line names (its stage profile's dominant one),
+# so that kernel's rocprof average and the line's live timer describe the same launches
+if [ -z "${TIMED:-}" ]; then
+  timeout -k 10 200 python3 $ROOT/bench.py --no-cpu-baseline --batch $BATCH --steps 4 --warmup 1 $ONLY \
+    > "$OUT/dominant_probe.json" 2> "$OUT/dominant_probe.err"
+  TIMED=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['dominant_kernel'])" "$OUT/dominant_probe.json")
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_timed" -o run -- \
-  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --timed-kernel ${TIMED:-k_blob_small} --batch $BATCH --steps 40 --warmup 3 $ONLY \
+  python3 $ROOT/bench.py --no-cpu-baseline --no-stage-profile --timed-kernel $TIMED --batch $BATCH --steps 40 --warmup 3 $ONLY \
   > "$OUT/trace_timed_bench.json" 2> "$OUT/trace_timed.err"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $SHORT \
   > /dev/null 2> "$OUT/pmc_fetch.err"
@@ -42,5 +49,5 @@ python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" "$OUT/p
 cp "$OUT/pmc_traffic.json" profiles/pmc_traffic.json  # the bench line below reads it
 python3 tools/pmc_agg.py "$OUT/pmc_sq_a/run_counter_collection.csv" "$OUT/pmc_sq_b/run_counter_collection.csv" > "$OUT/sq_counters_agg.txt"
 python3 tools/timed_launches.py "$OUT/trace_timed/run_kernel_trace.csv" "$OUT/trace_timed_bench.json" > "$OUT/timed_launches.json"
-timeout -k 10 400 python3 bench.py --batch $BATCH > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 400 python3 bench.py --batch $BATCH --timed-kernel $TIMED > "$OUT/bench.json" 2> "$OUT/bench.err"
 find "$OUT" -name "*.csv" | sort
