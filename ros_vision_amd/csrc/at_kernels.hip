@@ -1019,21 +1019,53 @@ __global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
       }
     }
     uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
+    // pair histogram: a pixel's (up to four) points nearly always share one pair,
+    // so a lane adds its first pair with the count of its points in it, runs of
+    // equal pairs in consecutive lanes sum their counts (wave scan), and only the
+    // rare other pairs of a lane go in one by one
+    uint64_t kp = 0;
+    uint32_t cnt = 0;
+    bool got = false;
 #pragma unroll
     for (int dir = 0; dir < 4; dir++) {
       const bool has = pk[dir] != 0;
       const uint64_t hmask = __ballot(has);
       below += lanes_below(hmask);
       wtot += (uint32_t)__popcll(hmask);
-      const uint64_t r01 = has ? (pk[dir] >> 24) : 0;
-      const uint64_t prev = wave_shr1_u64(r01);
-      const bool same = has && lane > 0 && prev == r01;
+      if (has) {
+        const uint64_t r01 = pk[dir] >> 24;
+        if (!got) kp = r01;
+        got = true;
+        cnt += r01 == kp;
+      }
+    }
+    {
+      const uint64_t prev = wave_shr1_u64(kp);
+      const bool same = got && lane > 0 && prev == kp;
       const uint64_t same_mask = __ballot(same);
-      if (has && !same) {
-        const uint32_t len = run_len(same_mask, lane);
-        if (!lds_pair_add(s_pkey, s_pcnt, r01, len)) {  // LDS table full
-          bnd_spill(b, f, r01, len);
+      const uint32_t incl = wave_incl_scan(cnt, AddOp(), 0u);
+      const bool head = got && !same;
+      const uint32_t len = head ? run_len(same_mask, lane) : 1u;
+      const uint32_t incl_end = (uint32_t)__shfl((int)incl, (int)(lane + len - 1));
+      if (head) {
+        const uint32_t tot = incl_end - incl + cnt;
+        if (!lds_pair_add(s_pkey, s_pcnt, kp, tot)) {  // LDS table full
+          bnd_spill(b, f, kp, tot);
           s_spill = 1;
+        }
+      }
+      bool extra = false;
+#pragma unroll
+      for (int dir = 0; dir < 4; dir++) extra |= pk[dir] != 0 && (pk[dir] >> 24) != kp;
+      if (__ballot(extra)) {
+#pragma unroll
+        for (int dir = 0; dir < 4; dir++) {
+          if (pk[dir] != 0 && (pk[dir] >> 24) != kp) {
+            if (!lds_pair_add(s_pkey, s_pcnt, pk[dir] >> 24, 1u)) {
+              bnd_spill(b, f, pk[dir] >> 24, 1u);
+              s_spill = 1;
+            }
+          }
         }
       }
     }
