@@ -94,13 +94,18 @@ int at_detect_batch(at_detector *d, const uint8_t *const *frames, int nframes, a
                     at_detection *out, int cap_per_frame, int *n_per_frame);
 
 /* Frames already resident in device memory: d_frames is a device pointer to
- * nframes frames laid out back to back (frame_stride bytes apart). */
+ * nframes frames laid out back to back (frame_stride bytes apart).  The kernels
+ * read the frames until the last stage (the decode samples luma from YUYV / GRAY8
+ * frames in place), so the buffer must stay unmodified until the call returns --
+ * for at_enqueue_device, until at_collect returns. */
 int at_detect_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt,
                      at_detection *out, int cap_per_frame, int *n_per_frame);
 
 /* Split-phase form of at_detect_device for pipelining: enqueue the batch on
  * the detector's stream and return immediately; at_collect waits for it and
- * runs the host tail (reconcile + sort by id). */
+ * runs the host tail (reconcile + sort by id).  d_frames must stay unmodified
+ * until at_collect returns (see at_detect_device): a producer that reuses the
+ * buffer must order its writes after at_collect, not after earlier work. */
 int at_enqueue_device(at_detector *d, const void *d_frames, size_t frame_stride, int nframes, at_pixfmt fmt);
 int at_collect(at_detector *d, at_detection *out, int cap_per_frame, int *n_per_frame);
 /* Split-phase form of at_detect_batch (camera-fed pipelines): the host-to-device

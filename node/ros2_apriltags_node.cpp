@@ -90,6 +90,15 @@ class ApriltagsAmdNode : public rclcpp::Node {
     RCLCPP_INFO(get_logger(), "%s", sched_log.c_str());
   }
 
+ // Teardown order: no more image callbacks, then the publisher-queue thread drained
+  // and joined while image_pub_ is still alive (its publish hook uses it), then the
+  // detector; only then the publishers (declared before core_, so destroyed after it).
+  ~ApriltagsAmdNode() override {
+    sub_.reset();
+    if (core_) core_->flush_images();
+    core_.reset();
+  }
+
  private:
   static apriltags_cuda::msg::TagDetectionArray to_msg(const std::vector<at_node::TagDetectionMsg>& v) {
     apriltags_cuda::msg::TagDetectionArray a;
@@ -130,12 +139,14 @@ class ApriltagsAmdNode : public rclcpp::Node {
     if (rc != AT_OK) RCLCPP_WARN(get_logger(), "at_detect: %s", at_strerror(rc));
   }
 
-  std::unique_ptr<at_node::DetectorCore> core_;
   int width_ = 0, height_ = 0;
   std::vector<uint8_t> packed_, image_;
-  rclcpp::Subscription<sensor_msgs::msg::Image>::SharedPtr sub_;
   rclcpp::Publisher<apriltags_cuda::msg::TagDetectionArray>::SharedPtr pose_pub_, camera_pose_pub_;
   rclcpp::Publisher<sensor_msgs::msg::Image>::SharedPtr image_pub_;
+  // after the publishers: destroyed first (members go in reverse order), so the
+  // publisher-queue thread never outlives image_pub_
+  std::unique_ptr<at_node::DetectorCore> core_;
+  rclcpp::Subscription<sensor_msgs::msg::Image>::SharedPtr sub_;
 };
 
 int main(int argc, char** argv) {

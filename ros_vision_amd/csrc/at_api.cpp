@@ -140,10 +140,14 @@ struct at_detector {
   double kd_ms;             // device-clock spans of the timed kernel (sum) and their count
   long long kd_n;
   uint32_t* h_ctrl;         // pinned copy of the control block
-  DevDetection* h_dets;     // pinned [det_cap]: the batch-wide candidate pool (mapped)
-  // results of the last collected batch: frame f's detections are the pool records
-  // res_idx[res_off[f] .. res_off[f] + res_n[f]) in id order (after reconcile)
-  std::vector<int> res_idx, res_off, res_n;
+  DevDetection* h_dets;     // pinned [B][kDetPoolPerFrame]: mirror of each frame's first candidates (mapped)
+  // results of the last collected batch: frame f's detections are the records
+  // res_base[f][res_idx[f * kMaxDets + i]], i < res_n[f], in id order (after reconcile);
+  // res_base[f] is the frame's host mirror, or res_ovf[f] (its candidates copied from
+  // HBM) when it had more than kDetPoolPerFrame
+  std::vector<int> res_idx, res_n;
+  std::vector<const DevDetection*> res_base;
+  std::vector<std::vector<DevDetection>> res_ovf;
   int last_nframes;
   int last_fmt;
   int last_gray;            // the last batch wrote the gray plane (AT_STAGE_GRAY)
@@ -172,6 +176,24 @@ struct at_detector {
   size_t prims_cap;
   uint32_t* d_last;
 };
+
+// Experiment and diagnostic knobs (stage cut-offs, grid / tile overrides, phase
+// probes, graph / fork switches) are read from the environment only by a build
+// with -DAT_EXPERIMENTS (`make exp`, the A/B tools' library): a product build
+// ignores the environment, so no variable can truncate the pipeline of a deployed
+// detector (the reference either detects or aborts, cuda_frc971.h:14-17).
+static const char* knob(const char* name) {
+#ifdef AT_EXPERIMENTS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+static int knob_int(const char* name, int dflt) {
+  const char* v = knob(name);
+  return v ? atoi(v) : dflt;
+}
 
 static int hip_fail(hipError_t e) {
   if (e != hipSuccess) {
@@ -289,11 +311,12 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.TW = g.Wd / 4; g.TH = g.Hd / 4;
   g.BW = g.Wd / 2; g.BH = g.Hd / 2;
   g.ctw = d->B < kWideBlobMaxBatch ? 32 : 64;
-  if (getenv("AT_CCL_TILE")) g.ctw = atoi(getenv("AT_CCL_TILE")) == 32 ? 32 : 64;
+  if (knob("AT_CCL_TILE")) g.ctw = knob_int("AT_CCL_TILE", 64) == 32 ? 32 : 64;
   // size classes of the workgroup-team blob kernel (the rest: one wave per blob);
   // latency mode gives the team blobs of more than 256 points too (its chain is
   // the slowest single blob)
-  g.nlarge = (g.ctw == 32 && getenv("AT_NLARGE")) ? atoi(getenv("AT_NLARGE")) : kNumLargeCls;  // (experiment knob)
+  g.nlarge = g.ctw == 32 ? std::max(kNumLargeCls, std::min(kNumCls, knob_int("AT_NLARGE", kNumLargeCls)))
+                        : kNumLargeCls;  // (experiment knob: 3..kNumCls)
   g.CTX = (g.Wd + g.ctw - 1) / g.ctw;
   g.CTY = (g.Hd + kCclTileH - 1) / kCclTileH;
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
@@ -301,7 +324,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
   g.ntb = g.BTX * g.BTY;
   g.bnd_region = kBndPts;
-  if (getenv("AT_BND_REGION")) g.bnd_region = std::max(kBndStage, std::min(kBndPts, atoi(getenv("AT_BND_REGION"))));  // experiment
+  g.bnd_region = std::max(kBndStage, std::min(kBndPts, knob_int("AT_BND_REGION", kBndPts)));  // (experiment knob)
   if (g.ntb > kMaxTilesPerFrame) {
     at_destroy(d);
     return AT_E_INVALID;
@@ -318,15 +341,15 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.refine_edges = cfg->refine_edges;
   p.fx = cam->fx; p.fy = cam->fy; p.cx = cam->cx; p.cy = cam->cy;
   p.k1 = cam->k1; p.k2 = cam->k2; p.p1 = cam->p1; p.p2 = cam->p2; p.k3 = cam->k3;
-  p.diag_stop = getenv("AT_DIAG_BLOB_STOP") ? atoi(getenv("AT_DIAG_BLOB_STOP")) : 0;
-  p.probe = getenv("AT_PHASE_PROBE") ? atoi(getenv("AT_PHASE_PROBE")) : 0;
+  p.diag_stop = knob_int("AT_DIAG_BLOB_STOP", 0);
+  p.probe = knob_int("AT_PHASE_PROBE", 0);
   p.taps = 0;  // debug taps off: at_set_debug_taps
-  p.wide_blob = getenv("AT_WIDE_BLOB") ? atoi(getenv("AT_WIDE_BLOB")) : 0;
-  p.pipe_stop = getenv("AT_DIAG_PIPE_STOP") ? atoi(getenv("AT_DIAG_PIPE_STOP")) : 0;
-  p.lblob_wg = getenv("AT_LBLOB_WG") ? std::max(16, atoi(getenv("AT_LBLOB_WG"))) : 0;  // experiment
-  p.sblob_wg = getenv("AT_SBLOB_WG") ? std::max(16, atoi(getenv("AT_SBLOB_WG"))) : 0;  // experiment
+  p.wide_blob = knob_int("AT_WIDE_BLOB", 0);
+  p.pipe_stop = knob_int("AT_DIAG_PIPE_STOP", 0);
+  p.lblob_wg = knob("AT_LBLOB_WG") ? std::max(16, knob_int("AT_LBLOB_WG", 0)) : 0;  // experiment
+  p.sblob_wg = knob("AT_SBLOB_WG") ? std::max(16, knob_int("AT_SBLOB_WG", 0)) : 0;  // experiment
   p.fam = family_desc(*fam);
-  d->use_graphs = !(getenv("AT_NO_GRAPH") && atoi(getenv("AT_NO_GRAPH")));
+  d->use_graphs = !knob_int("AT_NO_GRAPH", 0);
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {
     at_destroy(d);
     return AT_E_INVALID;
@@ -346,7 +369,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   // stream -- concurrency comes from several detector instances (batches in
   // flight), which then each need one hardware queue only.  AT_NO_FORK=1 forces
   // the single-stream form.
-  const bool fork = d->B < kWideBlobMaxBatch && !(getenv("AT_NO_FORK") && atoi(getenv("AT_NO_FORK")));
+  const bool fork = d->B < kWideBlobMaxBatch && !knob_int("AT_NO_FORK", 0);
   if (fork && hipStreamCreateWithFlags(&d->st2, hipStreamNonBlocking) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
   if (hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming) != hipSuccess) return fail(AT_E_HIP);
@@ -364,7 +387,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   (void)hipDeviceGetAttribute(&wclk, hipDeviceAttributeWallClockRate, d->device);
   d->wclk_khz = wclk > 0 ? (double)wclk : 100000.0;  // s_memrealtime: 100 MHz
   d->nblobwg = std::max(64, ncu * 2);
-  if (getenv("AT_BLOB_WG")) d->nblobwg = std::max(16, atoi(getenv("AT_BLOB_WG")));  // experiment: persistent grid size
+  if (knob("AT_BLOB_WG")) d->nblobwg = std::max(16, knob_int("AT_BLOB_WG", 0));  // experiment: persistent grid size
 
   const size_t B = (size_t)d->B;
   const size_t npix = (size_t)W * H, nd = (size_t)g.Wd * g.Hd, nt = (size_t)g.TW * g.TH * 2;
@@ -410,8 +433,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.wcap = (uint32_t)(B * kMaxPairs);
   b.work = (uint32_t*)dalloc((size_t)kNumCls * B * kMaxPairs * 4);
   b.probe = (uint64_t*)dalloc(kProbeWords * 8);
-  b.det_cap = (uint32_t)std::max<size_t>(kMaxDets, (size_t)kDetPoolPerFrame * B);
-  b.dets = (DevDetection*)dalloc(b.det_cap * sizeof(DevDetection));
+  b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
+  b.det_work = (uint32_t*)dalloc(B * kMaxDets * 4);
   b.quads = (QuadRecord*)dalloc(B * kMaxPairs * sizeof(QuadRecord));
   // control block: per-frame words, scalars, then (8-byte aligned) the timed
   // kernel's two wall-clock stamps and its finished-workgroup count
@@ -451,11 +474,12 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     return fail(AT_E_NOMEM);
   if (hipHostGetDevicePointer((void**)&b.frames, (void*)d->h_ftab, 0) != hipSuccess) return fail(AT_E_HIP);
-  d->res_idx.assign(b.det_cap, 0);
-  d->res_off.assign(B, 0);
+  d->res_idx.assign(B * kMaxDets, 0);
   d->res_n.assign(B, 0);
+  d->res_base.assign(B, nullptr);
+  d->res_ovf.resize(B);
   if (hipHostMalloc((void**)&d->h_ctrl, d->ctrl_words * 4, hipHostMallocMapped) != hipSuccess) return fail(AT_E_NOMEM);
-  if (hipHostMalloc((void**)&d->h_dets, b.det_cap * sizeof(DevDetection), hipHostMallocMapped) != hipSuccess)
+  if (hipHostMalloc((void**)&d->h_dets, B * kDetPoolPerFrame * sizeof(DevDetection), hipHostMallocMapped) != hipSuccess)
     return fail(AT_E_NOMEM);
   // device views of the mapped host result buffers (k_decode / k_pose write them)
   if (hipHostGetDevicePointer((void**)&b.hdets, d->h_dets, 0) != hipSuccess ||
@@ -715,32 +739,30 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   }
   const int B = d->B;
   int rc = AT_OK;
-  // group the pool's candidates by frame (counting sort, pool order kept)
+  // each frame's candidates: its slots 0 .. ndets[f] (the first kDetPoolPerFrame
+  // already in the host mirror; a frame with more is copied from HBM)
   const int nf = d->last_nframes;
-  const int total = (int)std::min<uint32_t>(d->h_ctrl[kCtlPerFrame * B + kCtlDetHead], d->d.det_cap);
-  int* idx = d->res_idx.data();
-  int* off = d->res_off.data();
   int* cnt = d->res_n.data();
-  for (int f = 0; f < nf; f++) cnt[f] = 0;
-  for (int i = 0; i < total; i++) cnt[d->h_dets[i].frame]++;
-  for (int f = 0, o = 0; f < nf; f++) {
-    off[f] = o;
-    o += cnt[f];
-    cnt[f] = 0;
-  }
-  for (int i = 0; i < total; i++) {
-    const int f = d->h_dets[i].frame;
-    idx[off[f] + cnt[f]++] = i;
-  }
   for (int f = 0; f < nf; f++) {
     const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
+    const int ncand = (int)std::min<uint32_t>(d->h_ctrl[kCtlNdets * B + f], kMaxDets);
+    int* idx = d->res_idx.data() + (size_t)f * kMaxDets;
     int n = 0;
     if (status & kStatusPairsCapped) rc = AT_E_CAPACITY;  // the first kMaxPairs pairs' detections are kept
     if (status & (kStatusPairsOverflow | kStatusHashFull | kStatusPointsOverflow | kStatusQuadsOverflow | kStatusDetsOverflow)) {
       rc = AT_E_CAPACITY;
     } else {
-      n = host_tail(d->h_dets, idx + off[f], cnt[f], out ? out + (size_t)f * cap_per_frame : nullptr,
-                    out ? cap_per_frame : 0);
+      const DevDetection* cand = d->h_dets + (size_t)f * kDetPoolPerFrame;
+      if (ncand > kDetPoolPerFrame) {
+        std::vector<DevDetection>& v = d->res_ovf[f];
+        v.resize(ncand);
+        HIPCHK(hipMemcpy(v.data(), d->d.dets + (size_t)f * kMaxDets, ncand * sizeof(DevDetection),
+                         hipMemcpyDeviceToHost));
+        cand = v.data();
+      }
+      d->res_base[f] = cand;
+      for (int i = 0; i < ncand; i++) idx[i] = i;
+      n = host_tail(cand, idx, ncand, out ? out + (size_t)f * cap_per_frame : nullptr, out ? cap_per_frame : 0);
     }
     cnt[f] = n;
     if (n_per_frame) n_per_frame[f] = n;
@@ -907,7 +929,7 @@ int at_poses(at_detector* d, int frame, at_pose* out, int cap) {
   if (!(d->prm.tag_size > 0)) return 0;
   const int n = d->res_n[frame];
   for (int i = 0; i < n && i < cap; i++) {
-    const DevDetection& v = d->h_dets[d->res_idx[d->res_off[frame] + i]];
+    const DevDetection& v = d->res_base[frame][d->res_idx[(size_t)frame * kMaxDets + i]];
     at_pose& p = out[i];
     p.id = v.id;
     memcpy(p.R, v.pose_R, sizeof(p.R));
@@ -921,7 +943,8 @@ int at_detections(at_detector* d, int frame, at_detection* out, int cap) {
   if (!d || frame < 0 || frame >= d->last_nframes || (cap > 0 && !out)) return AT_E_INVALID;
   if (d->pending) return AT_E_INVALID;
   const int n = d->res_n[frame];
-  for (int i = 0; i < n && i < cap; i++) write_detection(d->h_dets[d->res_idx[d->res_off[frame] + i]], out + i);
+  for (int i = 0; i < n && i < cap; i++)
+    write_detection(d->res_base[frame][d->res_idx[(size_t)frame * kMaxDets + i]], out + i);
   return n;
 }
 

@@ -86,11 +86,12 @@ constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config
 // the reference decodes every quad (apriltag_detect.cu:618-663).
 constexpr int kQuadCandPerFrame = kMaxPairs;  // accepted quads queued for decode, per frame
 constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections one frame can have (before reconcile)
-// Candidate detections live in one batch-wide pool filled through an atomic cursor
-// (DevBufs::det_head): max(kMaxDets, kDetPoolPerFrame * B) records, so one frame can
-// still reach kMaxDets while the pinned result buffer follows the batch's typical
-// count instead of B * kMaxDets (a pool that fills flags kStatusDetsOverflow on the
-// frames whose candidates did not fit).
+// Candidate detections: every frame owns kMaxDets records in HBM (frame f's k-th
+// candidate, k from the frame's own counter, at f * kMaxDets + k: no frame can take
+// another's slots, so what a frame returns depends on that frame alone).  The first
+// kDetPoolPerFrame of them are mirrored into the pinned, mapped host buffer as they
+// are written (zero-copy results); a frame with more candidates (pathological
+// inputs) has the rest copied from HBM at at_collect.
 constexpr int kDetPoolPerFrame = 128;
 constexpr int kMaxCodes = 1024;               // codebook entries (tag36h11: 587)
 constexpr int kMaxFamilyBits = 64;
@@ -142,6 +143,19 @@ struct Params {
   int gp_w, gp_h, gp_c;  // game-piece preprocessing output (at_gp_enable); gp_c == 0: off
 };
 constexpr int kProbeWords = 256;
+
+// The diagnostics above (stage cut-offs, phase probes) exist only in a build with
+// -DAT_EXPERIMENTS (`make exp`); in the product build they are compile-time off,
+// whatever Params holds.
+#ifdef AT_EXPERIMENTS
+#define AT_DIAG_STOP(prm, n) ((prm).diag_stop == (n))
+#define AT_PIPE_STOP(prm) ((prm).pipe_stop)
+#define AT_PROBE_ON(prm) ((prm).probe != 0)
+#else
+#define AT_DIAG_STOP(prm, n) false
+#define AT_PIPE_STOP(prm) 0
+#define AT_PROBE_ON(prm) false
+#endif
 
 // HIP events bracketing one kernel of the launch sequence (bench roofline).
 // With `split` set (graph replay), the launch sequence calls split(ctx, 0) before
@@ -223,15 +237,15 @@ struct DevBufs {
   uint32_t* pair_sel; // [B][kMaxPairs]  1 if SelectBlobs kept the pair
   uint32_t* work;     // [kNumCls][wcap] (frame << 16) | rank of candidate pairs, by size class
   uint32_t wcap;      // B * kMaxPairs
-  DevDetection* dets; // [det_cap] batch-wide pool of candidates (DevDetection::frame)
-  uint32_t det_cap;
-  uint32_t* det_head; // [1] pool cursor (control block)
+  DevDetection* dets; // [B][kMaxDets] candidates of each frame (slot f * kMaxDets + k)
+  uint32_t* det_work; // [B * kMaxDets] slots of the batch's candidates in claim order (k_pose's work list)
+  uint32_t* det_head; // [1] k_pose work-list cursor (control block)
   uint32_t* dec_done; // [1] finished k_decode workgroups (control block; latency mode's fused pose)
   // zero-copy results: the detections (k_decode, poses added by k_pose) and the
   // control block (copied by k_pose) are also written straight into the
   // caller-visible pinned host buffers (device pointers of mapped host memory),
   // which replaces two device-to-host copies per batch
-  DevDetection* hdets;  // [det_cap] host
+  DevDetection* hdets;  // [B][kDetPoolPerFrame] host mirror of each frame's first candidates
   uint32_t* hctrl;      // [ctrl_words] host
   uint32_t* ctrl;       // device control block base
   uint32_t ctrl_words;
@@ -239,7 +253,7 @@ struct DevBufs {
   // control block (zeroed every batch)
   uint32_t* npts;     // [B]
   uint32_t* npairs;   // [B]
-  uint32_t* ndets;    // [B] candidates per frame (pool entries + overflowed ones)
+  uint32_t* ndets;    // [B] candidates per frame (the frame's slot cursor)
   uint32_t* nquads;   // [B]
   uint32_t* status;   // [B]
   uint32_t* ncls;     // [kNumCls] candidate pairs per size class

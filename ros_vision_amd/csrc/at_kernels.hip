@@ -2643,10 +2643,10 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   const uint32_t lane = lane_id();
   // AT_PHASE_PROBE: accumulated wall-clock per phase (probe[64 + 16*(NT>64) + k]);
   // the accumulators live in the team's LDS, not in registers
-  if (prm.probe && tid == 0) S.t_last = S.t_item = wall_clock64();
+  if (AT_PROBE_ON(prm) && tid == 0) S.t_last = S.t_item = wall_clock64();
   bool big = false;
   auto phase = [&](int k) {  // accumulated per team, flushed once per kernel
-    if (prm.probe && tid == 0) {
+    if (AT_PROBE_ON(prm) && tid == 0) {
       if (k == 9) __builtin_amdgcn_s_waitcnt(0);  // the item's stores are acknowledged inside its own time
       const uint64_t now = wall_clock64();
       pacc[k] += (uint32_t)(now - S.t_last);
@@ -2725,7 +2725,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     team_bitonic_sort<uint64_t, NT>(S.keys, np2);
   }
   phase(2);
-  if (prm.diag_stop == 2) return;
+  if (AT_DIAG_STOP(prm, 2)) return;
 
   // ---- line-fit points (P7): blocked chunks, W from the decimated gradient,
   // sorted keys -> compact words in place; chunk sums -> exclusive team scan
@@ -2764,7 +2764,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   }
   team_sync<NT>();
   phase(3);
-  if (prm.diag_stop == 3) return;
+  if (AT_DIAG_STOP(prm, 3)) return;
 
   // ---- errors (K10 ErrorCalculator, restated per blob, cyclic): the window
   // [t0 - ksz, t0 + ksz] of the chunk's first point from two prefix lookups
@@ -2914,7 +2914,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     team_sync<NT>();
   }
   phase(5);
-  if (prm.diag_stop == 4) return;
+  if (AT_DIAG_STOP(prm, 4)) return;
   // ---- FitQuads (K11) --------------------------------------------------------
   const int cnt = (int)npk;
   if (tid < 16) {
@@ -2980,7 +2980,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   }
   team_sync<NT>();
   phase(7);
-  if (prm.diag_stop == 7) return;
+  if (AT_DIAG_STOP(prm, 7)) return;
   // 210 lexicographic combinations; each lane keeps its first minimum
   double err = DBL_MAX;
   uint32_t bt = 0xffffffffu;
@@ -3019,7 +3019,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       if (S.red_f64[i] < err || (S.red_f64[i] == err && S.red_idx[i] < bt)) { err = S.red_f64[i]; bt = S.red_idx[i]; }
   }
   phase(8);
-  if (prm.diag_stop == 8) return;
+  if (AT_DIAG_STOP(prm, 8)) return;
   const double best = err;
   if (bt >= 210) bt = 0;
   const bool valid = best < (double)(prm.max_line_fit_mse * (float)n);
@@ -3115,7 +3115,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     rec.accepted = ok;
     b.quads[(size_t)f * kMaxPairs + rank] = rec;  // slot = pair rank: no returning atomic
     pacc[21] += 1;  // FitQuads records of this team (batch statistics, one atomic per team at the end)
-    if (ok && prm.diag_stop != 5) {
+    if (ok && !AT_DIAG_STOP(prm, 5)) {
       qcand.frame = (uint32_t)f;
       qcand.rank = rank;
       const uint32_t ci = atomicAdd(b.nqcand + f, 1u);  // per-frame counters spread the contention
@@ -3125,7 +3125,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   }
   }
   phase(9);
-  if (prm.probe && tid == 0) {  // slowest item of this team (flushed at kernel end): ticks, points, phases
+  if (AT_PROBE_ON(prm) && tid == 0) {  // slowest item of this team (flushed at kernel end): ticks, points, phases
     const uint32_t dt = (uint32_t)(S.t_last - S.t_item);
     if (dt > S.slow_dt) {
       S.slow_dt = dt;
@@ -3319,7 +3319,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVE
 template <int NT, int CAP>
 __device__ __forceinline__ void probe_flush_slow(const DevBufs& b, const Params& prm, const BlobShared<NT, CAP>& S,
                                                  bool leader) {
-  if (!prm.probe || !leader || !S.slow_dt) return;
+  if (!AT_PROBE_ON(prm) || !leader || !S.slow_dt) return;
   atomicMax((unsigned long long*)&b.probe[NT == 64 ? 200 : 201], ((unsigned long long)S.slow_dt << 20) | S.slow_n);
   if (NT == 64) {
     for (int k = 0; k < 10; k++) atomicAdd((unsigned long long*)&b.probe[224 + k], (unsigned long long)S.slow_ph[k]);
@@ -3329,7 +3329,7 @@ __device__ __forceinline__ void probe_flush_slow(const DevBufs& b, const Params&
 
 __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm, const uint32_t* pacc, int base,
                                             bool leader) {
-  if (!prm.probe || !leader) return;
+  if (!AT_PROBE_ON(prm) || !leader) return;
   for (int k = 0; k < 10; k++) {
     if (pacc[k]) atomicAdd((unsigned long long*)&b.probe[base + k], (unsigned long long)pacc[k]);
     if (pacc[10 + k]) atomicAdd((unsigned long long*)&b.probe[base + 32 + k], (unsigned long long)pacc[10 + k]);
@@ -3620,7 +3620,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
   uint32_t pacc[21] = {0};
   uint64_t t_last = 0;
   auto phase = [&](int k) {
-    if (prm.probe && tid == 0) {
+    if (AT_PROBE_ON(prm) && tid == 0) {
       const uint64_t now = wall_clock64();
       if (k > 0) {
         pacc[k] += (uint32_t)(now - t_last);
@@ -3787,7 +3787,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
       team_sync<64>();
       phase(3);
     }
-    if (prm.diag_stop == 6) continue;
+    if (AT_DIAG_STOP(prm, 6)) continue;
     // ---- homography (quad_update_homographies / homography_compute2) -----------
     if (homography_wave(S.qc, S.A, S.H) != 0) continue;
     if (tid == 0) {
@@ -3991,13 +3991,17 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
           d.pose_err[0] = P.err[0];
           d.pose_err[1] = P.err[1];
         }
-        atomicAdd(b.ndets + f, 1u);
-        const uint32_t di = atomicAdd(b.det_head, 1u);
-        if (di < b.det_cap) {
-          b.dets[di] = d;
-          b.hdets[di] = d;  // (POSE: complete; else the pose fields follow from k_pose)
+        // the frame's own slot; the first kDetPoolPerFrame also to the host mirror
+        // (POSE: complete; else the pose fields follow from k_pose)
+        const uint32_t k = atomicAdd(b.ndets + f, 1u);
+        if (k < (uint32_t)kMaxDets) {
+          const uint32_t slot = (uint32_t)f * kMaxDets + k;
+          b.dets[slot] = d;
+          if (k < (uint32_t)kDetPoolPerFrame) b.hdets[(uint32_t)f * kDetPoolPerFrame + k] = d;
+          if (!POSE) b.det_work[atomicAdd(b.det_head, 1u)] = slot;
+        } else {
+          atomicOr(b.status + f, kStatusDetsOverflow);  // (more candidates than quads: unreachable)
         }
-        else atomicOr(b.status + f, kStatusDetsOverflow);
       }
     }
     team_sync<64>();
@@ -4093,23 +4097,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AT_POSE_WAVE
   // the host (replaces a device-to-host copy)
   if (blockIdx.x == 0)
     for (uint32_t w = threadIdx.x; w < b.ctrl_words; w += 64) b.hctrl[w] = b.ctrl[w];
-  // the batch's candidates, whatever their frame (the pool is batch-wide)
-  const uint32_t n = min(*b.det_head, b.det_cap);
+  // the batch's candidates, whatever their frame (k_decode's work list of slots)
+  const uint32_t n = *b.det_head;
   constexpr uint32_t kPer = WAVE ? 1 : 64 / kPoseLanes;  // detections per wave
   for (uint32_t i = blockIdx.x * kPer + (WAVE ? 0 : threadIdx.x / kPoseLanes); i < n;  // uniform across the quad
        i += gridDim.x * kPer) {
-    DevDetection& d = b.dets[i];
+    const uint32_t slot = b.det_work[i];
+    DevDetection& d = b.dets[slot];
     double R[9], t[3], err[2];
     pose::estimate_tag_pose<WAVE>(d.H, d.p, prm.fx, prm.fy, prm.cx, prm.cy, prm.tag_size, R, t, err, sub,
-                                  (prm.probe && i == 0 && threadIdx.x == 0) ? b.probe + 16 : nullptr);
+                                  (AT_PROBE_ON(prm) && i == 0 && threadIdx.x == 0) ? b.probe + 16 : nullptr);
     if (WAVE ? threadIdx.x == 0 : sub == 0) {
-      DevDetection& h = b.hdets[i];
 #pragma unroll
-      for (int k = 0; k < 9; k++) d.pose_R[k] = h.pose_R[k] = R[k];
+      for (int k = 0; k < 9; k++) d.pose_R[k] = R[k];
 #pragma unroll
-      for (int k = 0; k < 3; k++) d.pose_t[k] = h.pose_t[k] = t[k];
-      d.pose_err[0] = h.pose_err[0] = err[0];
-      d.pose_err[1] = h.pose_err[1] = err[1];
+      for (int k = 0; k < 3; k++) d.pose_t[k] = t[k];
+      d.pose_err[0] = err[0];
+      d.pose_err[1] = err[1];
+      const uint32_t f = slot / kMaxDets, k = slot % kMaxDets;
+      if (k < (uint32_t)kDetPoolPerFrame) {  // the host mirror
+        DevDetection& h = b.hdets[f * kDetPoolPerFrame + k];
+#pragma unroll
+        for (int j = 0; j < 9; j++) h.pose_R[j] = R[j];
+#pragma unroll
+        for (int j = 0; j < 3; j++) h.pose_t[j] = t[j];
+        h.pose_err[0] = err[0];
+        h.pose_err[1] = err[1];
+      }
     }
   }
 }
@@ -4274,7 +4288,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt) {
   int e = 0;
-  auto on = [&](int stage) { return prm.pipe_stop <= 0 || stage < prm.pipe_stop; };
+  auto on = [&](int stage) { return AT_PIPE_STOP(prm) <= 0 || stage < AT_PIPE_STOP(prm); };
   auto mark = [&]() {
     if (ev) (void)hipEventRecord(ev[e++], st);
   };
@@ -4338,7 +4352,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     mark();
   }
   tk(5, st, 0);
-  if (on(5)) hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, prm.probe);
+  if (on(5)) hipLaunchKernelGGL(k_pairs, dim3(B), dim3(1024), 0, st, b, g, AT_PROBE_ON(prm));
   tk(5, st, 1);
   mark();
   tk(6, st, 0);

@@ -146,6 +146,63 @@ def render_dots(width: int, height: int, seed: int, side: int = 20, pitch: int =
     return np.clip(np.rint(img), 0, 255).astype(np.uint8), n
 
 
+def render_edge_board(width: int, height: int, seed: int, codes=None, family: str = "tag36h11"):
+    """A board whose tags and blobs touch the right and bottom image borders: the
+    partial last tile column / row of every tiled kernel at geometries whose
+    decimated size is not a multiple of the tile (800x600 -> 400x300, the deployed
+    camera of system_config.json:21-25).  A tag board fills the frame; tags are
+    pasted with their quiet zone flush against the right edge, the bottom edge and
+    the bottom-right corner (and one cut by the right edge); dark bars and a
+    checker strip cross both borders.  Returns (gray, ids of the pasted tags)."""
+    rng = np.random.default_rng(seed)
+    codes = codes if codes is not None else _codes(family)
+    known = sorted(codes)
+    gray, truth = render_board(width, height, seed=seed, ntags=6, side_range=(56, 80), codes=codes, family=family)
+    img = gray.astype(np.float32)
+    ids = [t[0] for t in truth]
+    used = set(ids)
+    free = [k for k in known if k not in used]
+    rng.shuffle(free)
+    side = min(width, height) // 5
+
+    def tag_crop(s, tid, sd):
+        """One tag (quiet zone included) cropped to its bounding box."""
+        sub, _ = render_board(s, s, seed=sd, ntags=1, side_range=(0.55 * s,) * 2, ids=[tid], codes=codes,
+                              family=family, noise_sigma=0.0, background=128)
+        ys, xs = np.nonzero(sub != 128)
+        return sub[ys.min():ys.max() + 1, xs.min():xs.max() + 1].astype(np.float32)
+
+    # dark bars crossing the right border, light bars crossing the bottom one, a
+    # checker strip along the bottom rows (small blobs cut by the border)
+    for k in range(4):
+        yb = int(rng.integers(8, height - 40))
+        img[yb:yb + int(rng.integers(6, 20)), width - int(rng.integers(12, 60)):] = 20.0
+        xb = int(rng.integers(8, width - 40))
+        img[height - int(rng.integers(12, 60)):, xb:xb + int(rng.integers(6, 20))] = 235.0
+    yy, xx = np.mgrid[0:10, 0:width]
+    img[height - 10:, :] = np.where(((xx // 5) + (yy // 5)) & 1, 230.0, 25.0)
+    s = side
+    # (anchor x or None = right-flush, anchor y or None = bottom-flush, gap to the border)
+    spots = [(None, (height - s) // 3, 0), (width // 3, None, 1), (None, None, 2), (None, 2, 1)]
+    for (ax, ay, gap) in spots:
+        tid = free.pop()
+        crop = tag_crop(s, tid, int(rng.integers(1 << 30)))
+        h, w = crop.shape
+        x0 = width - w - gap if ax is None else ax
+        y0 = height - h - gap if ay is None else ay
+        region = img[y0:y0 + h, x0:x0 + w]
+        img[y0:y0 + h, x0:x0 + w] = np.where(crop != 128, crop, region)
+        ids.append(tid)
+    # a tag cut by the right border (its quads are partial: both sides must agree on them)
+    crop = tag_crop(s, free.pop(), seed + 1)
+    h, w = crop.shape
+    y0 = (2 * (height - s)) // 3
+    region = img[y0:y0 + h, width - w // 2:]
+    img[y0:y0 + h, width - w // 2:] = np.where(crop[:, :w // 2] != 128, crop[:, :w // 2], region)
+    img += rng.normal(0.0, 2.0, size=img.shape).astype(np.float32)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8), ids
+
+
 def to_yuyv(gray: np.ndarray) -> np.ndarray:
     """Pack a gray plane as YUYV 4:2:2 (Y0 U Y1 V) with U = V = 128."""
     h, w = gray.shape

@@ -75,3 +75,17 @@ def test_stage_names():
     names = names[:names.index("")]
     assert names[0] == "k_pre" and names[-1] == "k_pose" and L.at_stage_name(99) == b""
     assert {"k_extents", "k_blob_small", "k_blob", "k_decode"} <= set(names)
+
+
+def test_product_library_ignores_the_environment():
+    """The experiment knobs (AT_DIAG_PIPE_STOP, AT_DIAG_BLOB_STOP, AT_NO_GRAPH, grid and
+    tile overrides, ...) are compiled in only with -DAT_EXPERIMENTS (`make exp`): the
+    product library does not even import getenv, and names none of them."""
+    import subprocess
+    lib = os.path.join(ROOT, "ros_vision_amd", "libat_hip.so")
+    nm = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True, check=True).stdout
+    assert not re.search(r"\bgetenv\b|\bsecure_getenv\b", nm)
+    data = open(lib, "rb").read()
+    for knob in (b"AT_DIAG_PIPE_STOP", b"AT_DIAG_BLOB_STOP", b"AT_NO_GRAPH", b"AT_NO_FORK", b"AT_CCL_TILE",
+                 b"AT_PHASE_PROBE", b"AT_BLOB_WG", b"AT_NLARGE", b"AT_BND_REGION", b"AT_WIDE_BLOB"):
+        assert knob not in data, knob

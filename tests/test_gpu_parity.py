@@ -116,6 +116,33 @@ def test_1080p_parity(gpu, oracle_mod):
     assert compare_detections(dets, orc.detections()) == []
 
 
+@pytest.mark.parametrize("W,H", [(800, 600), (1000, 600), (648, 488), (1352, 760), (816, 616)])
+@pytest.mark.parametrize("batch", [1, 8])
+def test_partial_tile_geometries(gpu, oracle_mod, W, H, batch):
+    """Decimated planes that are not a multiple of any tile (800x600 is the deployed
+    camera of system_config.json:21-25: 400x300 against 32/64-wide CCL tiles, 32-row
+    CCL tiles and 64x16 boundary tiles); tags and blobs flush against the right and
+    bottom borders.  The reference's only geometry preconditions are W, H multiples of
+    8 (threshold.cu:156-157) and even decimated sizes (labeling_allegretti_2019_BKE.cu:
+    469-475).  Latency mode (batch 1: 32-wide CCL tiles, k_pre fused) and throughput
+    mode (batch 8: 64-wide tiles, k_extents, k_ccl_keep): every stage bit-exact."""
+    from ros_vision_amd import synth
+    codes = dict(oracle_mod.family_entries())
+    frames = [synth.render_edge_board(W, H, seed=W + H + 7 * k, codes=codes) for k in range(min(batch, 3))]
+    fmt = gpu.AT_FMT_GRAY8 if W % 16 == 0 else gpu.AT_FMT_YUYV
+    inputs = [g if fmt == gpu.AT_FMT_GRAY8 else synth.to_yuyv(g) for g, _ in frames]
+    det = gpu.GpuDetector(W, H, max_batch=batch)
+    res = det.detect_batch(inputs, fmt)
+    ndet = 0
+    for c, f in enumerate(inputs):
+        orc = oracle_mod.Oracle(W, H)
+        orc.detect(f, fmt)
+        assert compare_frame(det, orc, frame_idx=c) == [], (W, H, batch, c)
+        assert compare_detections(res[c], orc.detections()) == [], (W, H, batch, c)
+        ndet += len(res[c])
+    assert ndet >= 6 * len(inputs)
+
+
 def test_bgr_and_gray_inputs(gpu, oracle_mod):
     from ros_vision_amd import synth
     gray, _ = synth.render_board(640, 480, seed=766, ntags=4)
@@ -372,3 +399,60 @@ def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     det.set_profiling(False)
     assert nb >= 2 and all(v > 0 for v in stages.values())
     assert run() == base
+
+
+def test_environment_cannot_truncate_the_pipeline(oracle_mod):
+    """A deployed detector with the former diagnostic knobs set (stage cut-offs, no
+    graphs, other grids) still returns the oracle's detections: the product library
+    ignores the environment (the reference either detects or aborts,
+    cuda_frc971.h:14-17).  Run in a child process so the variables are seen from
+    the first HIP call."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from ros_vision_amd import synth
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, AT_DIAG_PIPE_STOP="3", AT_DIAG_BLOB_STOP="2", AT_NO_GRAPH="1", AT_CCL_TILE="32",
+               AT_BLOB_WG="16", AT_NLARGE="0", AT_BND_REGION="1")
+    env.pop("AT_HIP_LIB", None)
+    code = ("import json, sys; sys.path.insert(0, %r)\n"
+            "import ros_vision_amd as rva\nfrom ros_vision_amd import synth\n"
+            "out = []\n"
+            "for b in (1, 8):\n"
+            "    det = rva.GpuDetector(1280, 720, max_batch=b)\n"
+            "    out.append([d.id for d in det.detect(synth.stream_frame(1280, 720, 4)[0])])\n"
+            "print(json.dumps(out))\n" % root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    orc = oracle_mod.Oracle(1280, 720)
+    orc.detect(synth.stream_frame(1280, 720, 4)[0], 0)
+    want = [d["id"] for d in orc.detections()]
+    assert len(want) == 15 and got == [want, want]
+
+
+@pytest.mark.parametrize("batch", [4, 8])
+def test_dense_frames_keep_every_candidate(gpu, oracle_mod, batch):
+    """Each frame owns its candidate slots (kMaxDets per frame in HBM, the first 128
+    mirrored to the host; more copied at collect): a batch of frames with more than
+    128 detections each returns every frame's detections, as the reference keeps every
+    detection (apriltag_detect.cu:618-663), whatever the other frames hold."""
+    from ros_vision_amd import synth
+    codes = dict(oracle_mod.family_entries())
+    frames = []
+    for k in range(3):
+        g, _ = synth.render_board(1920, 1080, seed=9160 + k, ntags=160, side_range=(50, 64),
+                                  ids=[(400 + 3 * k + j) % 587 for j in range(160)], codes=codes)
+        frames.append(synth.to_yuyv(g))
+    frames.append(synth.stream_frame(1920, 1080, 3)[0])
+    det = gpu.GpuDetector(1920, 1080, max_batch=batch)
+    res = det.detect_batch(frames)
+    for c, f in enumerate(frames):
+        assert det.frame_status(c) == 0
+        orc = oracle_mod.Oracle(1920, 1080)
+        orc.detect(f, 0)
+        assert compare_detections(res[c], orc.detections()) == [], c
+        if c < 3:
+            assert len(res[c]) > 128
+        assert len(det.poses(c)) == len(res[c])

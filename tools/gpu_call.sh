@@ -20,13 +20,13 @@ fi
 if [ -n "${LAT_ENVS:-}" ]; then
   for r in 1 2; do for ev in $LAT_ENVS; do
     echo "== $ev" >> $O/lat_env.txt
-    env $ev timeout -k 10 120 python tools/lat_stages.py 300 2>&1 | grep wall >> $O/lat_env.txt || exit 1
+    env AT_HIP_LIB=${AT_HIP_LIB:-ros_vision_amd/ab/libat_hip_exp.so} $ev timeout -k 10 120 python tools/lat_stages.py 300 2>&1 | grep wall >> $O/lat_env.txt || exit 1
   done; done
 fi
 if [ -n "${C3_ENVS:-}" ]; then
   for r in 1 2; do for ev in $C3_ENVS; do
     echo -n "round=$r $ev " >> $O/c3_env.txt
-    env $ev timeout -k 10 200 python bench.py --steps 10 --no-cpu-baseline --no-stage-profile --host-ingest-steps 0 --latency-frames 500 \
+    env AT_HIP_LIB=${AT_HIP_LIB:-ros_vision_amd/ab/libat_hip_exp.so} $ev timeout -k 10 200 python bench.py --steps 10 --no-cpu-baseline --no-stage-profile --host-ingest-steps 0 --latency-frames 500 \
       2>>$O/err.txt | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['p50_latency_ms'], j['p50_latency_hbm_ms'], j['p50_latency_c3_ms'])" >> $O/c3_env.txt || exit 1
   done; done
 fi

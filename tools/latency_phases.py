@@ -7,6 +7,9 @@ import sys
 import numpy as np
 
 os.environ.setdefault("AT_PHASE_PROBE", "1")
+# the phase probes exist only in the experiment build (make -C ros_vision_amd/csrc exp)
+os.environ.setdefault("AT_HIP_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                 "ros_vision_amd/ab/libat_hip_exp.so"))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import ros_vision_amd as rva  # noqa: E402

@@ -43,6 +43,12 @@ def cases():
         codes=codes)[0]), T
     # more accepted quads than the former 512-quad decode queue
     yield "dots_1080p", 1920, 1080, 2, synth.render_dots(1920, 1080, seed=9512)[0], T
+    # geometries whose decimated plane is not a multiple of the CCL / boundary tiles
+    # (800x600: the deployed camera of system_config.json:21-25, W/2 = 400, H/2 = 300),
+    # with tags and blobs flush against the right and bottom borders
+    for (W, H, fmt) in ((800, 600, 2), (1000, 600, 0), (648, 488, 0), (1352, 760, 2)):
+        g8 = synth.render_edge_board(W, H, seed=W + H, codes=codes)[0]
+        yield "edge_%dx%d" % (W, H), W, H, fmt, (g8 if fmt == 2 else synth.to_yuyv(g8)), T
     # the other classic families (apriltag_utils.cu:13-16): every code of the family on
     # two 720p boards (tag16h5 also decodes texture quads, as upstream does)
     for fam, n in (("tag25h9", 35), ("tag16h5", 30)):
