@@ -191,7 +191,9 @@ int at_kernel_span(at_detector *d, double *avg_ms, long long *launches);
  * [2] blob pairs, [3] points processed by the small-blob kernel, [4] by the
  * large-blob kernel, [5] fitted quads, [6] decoded candidates (pre-reconcile);
  * host time of this detector since creation, microseconds: [7] waiting in
- * at_collect for the GPU, [8] in the host tail (reconcile, sort, poses).
+ * at_collect for the GPU, [8] in the host tail (reconcile, sort, poses);
+ * CCL: [9] local roots listed for the cross-tile merge (all frames), [10] their
+ * maximum over the frames, [11] frames merged by the multi-workgroup fallback.
  * Returns the number of entries written. */
 int at_batch_stats(at_detector *d, uint64_t *out, int cap);
 

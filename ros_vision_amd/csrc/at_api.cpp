@@ -27,6 +27,7 @@ hipError_t launch_tap_sizes(const uint8_t* thr, const uint32_t* par, const uint3
 hipError_t launch_tap_labels(const uint8_t* thr, const uint32_t* par, uint32_t* out, int Wd, int Hd, hipStream_t st);
 hipError_t launch_gp_preprocess(const uint8_t* src, int w, int h, float* out, int ow, int oh, int c, hipStream_t st);
 hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bgr, int W, int H, hipStream_t st);
+hipError_t prepare_kernels(const Geom& g);
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt);
@@ -111,7 +112,8 @@ using namespace at;
 
 // control block layout (u32 words, zeroed every batch): per-frame arrays of B
 // words, then scalars
-enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlPerFrame };
+enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlCclOvf, kCtlNlr,
+       kCtlPerFrame };
 enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
        kCtlDetHead = kCtlNcls + kNumCls, kCtlDecDone = kCtlDetHead + 1, kCtlScalars = kCtlDecDone + 1 };
 
@@ -319,6 +321,15 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
                         : kNumLargeCls;  // (experiment knob: 3..kNumCls)
   g.CTX = (g.Wd + g.ctw - 1) / g.ctw;
   g.CTY = (g.Hd + kCclTileH - 1) / kCclTileH;
+  // throughput mode: the cross-tile merge of the CCL in one workgroup's LDS per
+  // frame (k_ccl_merge), room for 80 listed local roots per tile (typical 720p
+  // frames list ~40), at most what 160 KiB hold; latency mode keeps the
+  // multi-workgroup border / roots kernels (one frame: their parallelism is the chain)
+  g.merge_cap = g.ctw == 64 ? std::min(kMergeCapMax, 80 * g.CTX * g.CTY) : 0;
+  if (g.CTX * g.CTY > kMaxCclTiles) {
+    at_destroy(d);
+    return AT_E_INVALID;
+  }
   g.cap_pts = 4 * (g.Wd - 2) * (g.Hd - 2);
   g.BTX = (g.Wd - 2 + 63) / 64;
   g.BTY = (g.Hd - 2 + 4 * kBndRows - 1) / (4 * kBndRows);
@@ -411,6 +422,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.par = (uint32_t*)dalloc(B * nd * 4);
   b.lroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodesMax * 4);
   b.nlroot = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * 4);
+  b.lcnt = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * kCclTileNodesMax * 4);
+  b.cdesc = (uint32_t*)dalloc(B * (size_t)g.CTX * g.CTY * CclDesc::kWords * 4);
   b.size = (uint32_t*)dalloc(B * nd * 4);
   const size_t ntb = (size_t)g.ntb;
   b.pts = (uint64_t*)dalloc(B * ntb * (size_t)g.bnd_region * 8);
@@ -448,6 +461,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.status = d->d_ctrl + kCtlStatus * B;
   b.npent = d->d_ctrl + kCtlNpent * B;
   b.nqcand = d->d_ctrl + kCtlNqcand * B;
+  b.ccl_ovf = d->d_ctrl + kCtlCclOvf * B;
+  b.nlr_tot = d->d_ctrl + kCtlNlr * B;
   uint32_t* sc = d->d_ctrl + kCtlPerFrame * B;
   b.workhead = sc + kCtlWorkhead;
   b.qhead = sc + kCtlQhead;
@@ -469,6 +484,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   // launch_pipeline uses for a full batch (decode_grid)
   b.rsamp = (double*)dalloc((size_t)decode_grid(d->nblobwg, d->B) * 2 * (kMaxRefineSamples - kLdsRefine) * 8);
   if (oom) return fail(AT_E_NOMEM);
+  if (prepare_kernels(g) != hipSuccess) return fail(AT_E_HIP);
   // frame pointer table: fine-grained mapped host memory read by k_pre directly
   // (no host-to-device copy per batch; the GPU does not cache it)
   if (hipHostMalloc((void**)&d->h_ftab, B * sizeof(void*), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
@@ -906,19 +922,22 @@ int at_batch_stats(at_detector* d, uint64_t* out, int cap) {
   if (!d || !out || cap < 1) return AT_E_INVALID;
   if (d->pending) return AT_E_INVALID;
   const int B = d->B;
-  uint64_t v[9] = {0};
+  uint64_t v[12] = {0};
   v[0] = (uint64_t)d->last_nframes;
   for (int f = 0; f < d->last_nframes; f++) {
     v[1] += d->h_ctrl[kCtlNpts * B + f];
     v[2] += d->h_ctrl[kCtlNpairs * B + f];
     v[6] += d->h_ctrl[kCtlNdets * B + f];
+    v[9] += d->h_ctrl[kCtlNlr * B + f];
+    v[10] = std::max<uint64_t>(v[10], d->h_ctrl[kCtlNlr * B + f]);
+    v[11] += d->h_ctrl[kCtlCclOvf * B + f] != 0;
   }
   v[5] = d->h_ctrl[kCtlNquads * B];  // FitQuads records of the batch (counted per blob team)
   v[3] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts];
   v[4] = d->h_ctrl[kCtlPerFrame * B + kCtlBlobPts + 1];
   v[7] = (uint64_t)d->host_wait_us;
   v[8] = (uint64_t)d->host_tail_us;
-  const int n = std::min(cap, 9);
+  const int n = std::min(cap, 12);
   for (int i = 0; i < n; i++) out[i] = v[i];
   return n;
 }

@@ -40,6 +40,21 @@ constexpr int kLdsPairSlots = 512;
 // tcnt flag: the tile's points are 4-B (entry index, point bits) words (k_boundary)
 constexpr uint32_t kTileNarrow = 0x80000000u;
 constexpr int kMaxTilesPerFrame = 1024;  // k_boundary tiles of one frame (k_pairs' LDS prefix); 1080p: 510
+constexpr int kMaxCclTiles = 1024;       // CCL tiles of one frame (k_ccl_merge: one per thread)
+// Border descriptor of a throughput-mode CCL tile (64 x 32 decimated pixels, 32 x 16
+// blocks), written by k_thr_ccl, read by k_ccl_merge; u32 word offsets.  *thr:
+// threshold bytes of row 0 (T), row 31 (B), column 0 (L), column 63 (R); *s?: the
+// list slot (u16, 0xffff: no pixels) of the root of node F / L / R of each block of
+// the top row, bottom row, left and right block column.
+struct CclDesc {
+  static constexpr int Tthr = 0, Bthr = 16, Lthr = 32, Rthr = 40;
+  static constexpr int TsF = 48, TsL = 64, TsR = 80, BsF = 96, BsL = 112, BsR = 128;
+  static constexpr int LsF = 144, LsL = 152, RsF = 160, RsR = 168;
+  static constexpr int kWords = 176;
+};
+// k_ccl_merge's LDS: 14 B per listed local root (parent key, pixel count, tile)
+// next to the per-tile prefix, within the 160 KiB one workgroup may hold
+constexpr int kMergeCapMax = 11264;
 constexpr int kMaxPairs = 4096;        // 12-bit blob index of IndexPoint (points.h:183-193)
 constexpr int kSortCap = 8192;         // points of one blob sorted in LDS (>= 2*(W+H) for 1080p)
 constexpr int kBlobThreads = 256;
@@ -63,7 +78,7 @@ inline int decode_grid(int nblobwg, int B) {
 
 // ---- stages of one launch sequence (per-stage event timing) ----------------
 constexpr int kNumStages = 12;
-constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_border", "k_ccl_roots",
+constexpr const char* kStageNames[kNumStages] = {"k_pre",   "k_thr_ccl", "k_ccl_merge", "k_ccl_roots",
                                                  "k_boundary", "k_pairs", "k_group",     "k_extents",
                                                  "k_blob_small", "k_blob", "k_decode",   "k_pose"};
 
@@ -115,6 +130,7 @@ struct Geom {
   int BW, BH;           // 2x2 CCL blocks
   int CTX, CTY;         // CCL tiles
   int ctw;              // CCL tile width (32: latency mode, 64: throughput mode)
+  int merge_cap;        // k_ccl_merge: listed local roots one frame's LDS holds (0: no k_ccl_merge)
   int nlarge;           // size classes 0 .. nlarge-1 go to the workgroup-team blob kernel
   int bnd_region;       // points per k_boundary tile region (kBndPts)
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)
@@ -214,6 +230,12 @@ struct DevBufs {
   uint32_t* par;      // [B][Wd*Hd]     union-find parents indexed by node id
   uint32_t* lroot;    // [B][CTX*CTY][kCclTileNodesMax] local roots of each CCL tile (global node ids)
   uint32_t* nlroot;   // [B][CTX*CTY]
+  uint32_t* lcnt;     // [B][CTX*CTY][kCclTileNodesMax] pixel count of each listed local root
+  uint32_t* cdesc;    // [B][CTX*CTY][CclDesc::kWords] border descriptors (throughput mode)
+  uint32_t* ccl_ovf;  // [B] (control block) frames whose listed local roots exceeded k_ccl_merge's LDS:
+                      //     k_ccl_border / k_ccl_roots / k_ccl_keep resolve them (every frame when
+                      //     merge_cap == 0)
+  uint32_t* nlr_tot;  // [B] (control block) listed local roots of the frame (k_ccl_merge; statistics)
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order
   uint32_t* tcnt;     // [B][ntb]        points of each tile

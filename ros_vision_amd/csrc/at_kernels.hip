@@ -72,6 +72,12 @@ __device__ __forceinline__ T wave_incl_scan(T x, Op op, T id) {
   return x;
 }
 
+// Value of lane l-1 in lane l (lane 0: `fill`): one DPP wave_shr:1 move per
+// dword instead of a ds_bpermute round trip through LDS.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 // value of lane + 1 (lane 63: 0): DPP wave_shl:1
 __device__ __forceinline__ uint32_t wave_read_next(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
@@ -335,10 +341,16 @@ struct BorderRoles {
 // kept bit of a root's parent word: the component has >= 25 pixels (BlobDiff's
 // size test, apriltag_gpu.cu:331-337), throughput mode
 constexpr uint32_t kKeptBit = 0x80000000u;
+// par word of a listed local root between k_thr_ccl and k_ccl_merge (throughput
+// mode): kListBit | its slot in the tile's list (node ids are < 2^22)
+constexpr uint32_t kListBit = 0x40000000u;
 // s_cnt flag of a local root whose component reaches a border block of the tile
 // (only those can take part in k_ccl_border's unions)
 constexpr uint32_t kTouchBit = 0x80000000u;
 
+#ifndef AT_TC_EXP
+#define AT_TC_EXP 0  // (cost attribution builds only)
+#endif
 // PRE < 0: the tile's decimated pixels and 4x4 min/max come from k_pre's planes.
 // PRE = 0 / 1 / 2 (frame format YUYV / BGR8 / GRAY8): k_pre's work is done here --
 // the workgroup reads its tile's full-resolution rows once (gray and decimated
@@ -365,6 +377,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   __shared__ uint32_t s_par[kCclTileNodes];
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
+  __shared__ uint16_t s_li[TWD == 64 ? kCclTileNodes : 1];  // list slot of each listed root (border descriptor)
   if (tid == 0) s_nlr = 0;
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
@@ -384,6 +397,17 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     }
   }
   kt_begin(b, 1);
+  // AT_PHASE_PROBE (throughput mode): per-phase wall-clock of workgroup thread 0
+  // summed over the launch in probe[48 + k], workgroups in probe[63]
+  uint64_t t_ph = 0;
+  auto ph = [&](int k) {
+    if (!AT_PROBE_ON(prm) || PRE >= 0 || tid != 0) return;
+    const uint64_t t = wall_clock64();
+    if (k > 0) atomicAdd((unsigned long long*)&b.probe[47 + k], (unsigned long long)(t - t_ph));
+    else atomicAdd((unsigned long long*)&b.probe[63], 1ull);
+    t_ph = t;
+  };
+  ph(0);
   if constexpr (PRE >= 0) {
     const uint8_t* in = b.frames[f];
     uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
@@ -489,6 +513,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     s_umx[r][c] = mx;
   }
   __syncthreads();
+  ph(1);
   }
   // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+kTH-1
   for (int i = tid; i < (kTH + 1) * (kTW + 2); i += NT) {
@@ -505,6 +530,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     s_fmx[r][c] = mx;
   }
   __syncthreads();
+  ph(2);
   // InternalThreshold for the halo region; outside the image -> 127
 #pragma unroll
   for (int k = 0; k < kDecPer; k++) {
@@ -528,6 +554,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   }
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
   __syncthreads();
+  ph(3);
   // write this tile's threshold plane (4 bytes per thread)
   {
     const int r = tid / (kCclTileW / 4), c4 = (tid % (kCclTileW / 4)) * 4;
@@ -574,6 +601,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     s_par[L] = hL;
     s_par[R] = hR;
     __syncthreads();
+  ph(4);
     // heads of the run(s) above this block's vertical links (read before any union)
     constexpr uint32_t kNone = 0xffffffffu;
     uint32_t tUL = kNone, tU = kNone, tUR = kNone, tL = kNone, tR = kNone;
@@ -588,6 +616,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     // the left neighbour's targets (same wave: rows never straddle waves)
     const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
     __syncthreads();
+  ph(5);
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
     if (tU != kNone && tU != tUL && !seen_fg(tU)) lds_union(s_par, hF, tU);
@@ -597,8 +626,10 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   }
 #undef T
   __syncthreads();
+  ph(6);
   const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
   __syncthreads();
+  ph(7);
   s_par[F] = rF;
   s_par[L] = rL;
   s_par[R] = rR;
@@ -615,6 +646,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     if (nbr) atomicOr(&s_cnt[rR], kTouchBit);
   }
   __syncthreads();
+  ph(8);
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
   if (BY < g.BH && BX < g.BW) {
@@ -640,23 +672,81 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     auto fin = [&](uint32_t w, uint32_t c) -> uint32_t {
       return (kKeep && c && !(w & kTouchBit) && c >= 25) ? kKeptBit : 0u;
     };
-    *reinterpret_cast<uint2*>(par + idF) = make_uint2(gid(rF) | fin(wF, cF), idF + 1);
-    *reinterpret_cast<uint2*>(par + idL) = make_uint2(gid(rL) | fin(wL, cL), gid(rR) | fin(wR, cR));
+    // the tile's local roots of components reaching its border (with pixels), for
+    // the cross-tile merge (k_ccl_merge; k_ccl_border / k_ccl_roots / k_ccl_keep)
+    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+    uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
+    const bool lF = cF && (wF & kTouchBit), lL = cL && (wL & kTouchBit), lR = cR && (wR & kTouchBit);
+    const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
+                   iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
+    uint32_t* lc = b.lcnt + tl * kCclTileNodesMax;
+    if (lF) { lr[iF] = gid(F); if (!(AT_TC_EXP & 2)) lc[iF] = cF; }
+    if (lL) { lr[iL] = gid(L); if (!(AT_TC_EXP & 2)) lc[iL] = cL; }
+    if (lR) { lr[iR] = gid(R); if (!(AT_TC_EXP & 2)) lc[iR] = cR; }
+    if constexpr (kKeep && !(AT_TC_EXP & 4)) {  // list slots of the roots, for the border descriptor
+      if (lF) s_li[F] = (uint16_t)iF;
+      if (lL) s_li[L] = (uint16_t)iL;
+      if (lR) s_li[R] = (uint16_t)iR;
+    }
+    // throughput mode: a listed root's own word names its list slot (kListBit | slot)
+    // until k_ccl_merge overwrites it with the component's root (the merge finds a
+    // node's slot in two hops: node -> local root -> slot)
+    auto word = [&](uint32_t r, uint32_t w, uint32_t c, bool listed, uint32_t li) -> uint32_t {
+      return (kKeep && listed) ? kListBit | li : gid(r) | fin(w, c);
+    };
+    *reinterpret_cast<uint2*>(par + idF) = make_uint2(word(rF, wF, cF, lF, iF), idF + 1);
+    *reinterpret_cast<uint2*>(par + idL) = make_uint2(word(rL, wL, cL, lL, iL), word(rR, wR, cR, lR, iR));
     if (cF) size[idF] = cF;
     if (cL | cR) {
       if (cL && cR) *reinterpret_cast<uint2*>(size + idL) = make_uint2(cL, cR);
       else if (cL) size[idL] = cL;
       else size[idL + 1] = cR;
     }
-    // the tile's local roots of components reaching its border (with pixels), for
-    // k_ccl_roots / k_ccl_keep
-    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
-    uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-    if (cF && (wF & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(F);
-    if (cL && (wL & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(L);
-    if (cR && (wR & kTouchBit)) lr[atomicAdd(&s_nlr, 1u)] = gid(R);
   }
   __syncthreads();
+  ph(9);
+  if constexpr (TWD == 64 && !(AT_TC_EXP & 1)) {
+    // throughput mode: the tile's border descriptor for k_ccl_merge (CclDesc) --
+    // the threshold bytes of its outer rows / columns and the list slots of the
+    // roots of its border blocks' nodes (a node with pixels in a border block
+    // belongs to a listed root), so the merge reads whole descriptors instead of
+    // scattered threshold bytes and parent words
+    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+    uint32_t* dw = b.cdesc + tl * CclDesc::kWords;
+    uint16_t* dh = reinterpret_cast<uint16_t*>(dw);
+    auto slot = [&](uint32_t n, uint32_t r) -> uint16_t { return n ? s_li[r] : (uint16_t)0xffffu; };
+    if (bty == 0) {
+      dh[2 * CclDesc::TsF + btx] = slot(nfg, rF);
+      dh[2 * CclDesc::TsL + btx] = slot(nbl, rL);
+      dh[2 * CclDesc::TsR + btx] = slot(nbr, rR);
+    }
+    if (bty == CT::BH - 1) {
+      dh[2 * CclDesc::BsF + btx] = slot(nfg, rF);
+      dh[2 * CclDesc::BsL + btx] = slot(nbl, rL);
+      dh[2 * CclDesc::BsR + btx] = slot(nbr, rR);
+    }
+    if (btx == 0) {
+      dh[2 * CclDesc::LsF + bty] = slot(nfg, rF);
+      dh[2 * CclDesc::LsL + bty] = slot(nbl, rL);
+    }
+    if (btx == kCclBW - 1) {
+      dh[2 * CclDesc::RsF + bty] = slot(nfg, rF);
+      dh[2 * CclDesc::RsR + bty] = slot(nbr, rR);
+    }
+    // threshold bytes (127 outside the image): rows 0 and 31, columns 0 and 63
+    auto row4 = [&](int r, int c) -> uint32_t {  // (byte reads: the rows start at odd offsets)
+      return s_t[r][c] | (s_t[r][c + 1] << 8) | (s_t[r][c + 2] << 16) | ((uint32_t)s_t[r][c + 3] << 24);
+    };
+    if (tid < 16) {
+      dw[CclDesc::Tthr + tid] = row4(1, 1 + 4 * tid);
+    } else if (tid < 32) {
+      dw[CclDesc::Bthr + tid - 16] = row4(kCclTileH, 1 + 4 * (tid - 16));
+    } else if (tid < 48) {
+      const int k = tid - 32, c = k < 8 ? 1 : kCclTileW, r = 1 + 4 * (k & 7);
+      dw[(k < 8 ? CclDesc::Lthr : CclDesc::Rthr) + (k & 7)] =
+          s_t[r][c] | (s_t[r + 1][c] << 8) | (s_t[r + 2][c] << 16) | ((uint32_t)s_t[r + 3][c] << 24);
+    }
+  }
   if (tid == 0) {
     b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
     kt_end(b, 1);
@@ -727,8 +817,9 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
   constexpr int kBorderTop = BorderRoles<TWD>::Top, kBorderLeft = BorderRoles<TWD>::Left,
                 kBorderRight = BorderRoles<TWD>::Right;
   constexpr int kCclBW = CclTile<TWD>::BW, kCclBH = CclTile<TWD>::BH;
-  kt_begin(b, 2);
   const int f = blockIdx.z;
+  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
+  if (!g.merge_cap) kt_begin(b, 2);
   const int t = threadIdx.x;
   int bty = 0, btx = 0, role = 3, kind = 0;  // role 3: no candidate (padding threads)
   if (t < kBorderTop) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
@@ -774,7 +865,7 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
     link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
   }
   if (link) g_union2(par, u, v);
-  if (b.kt_stage == 2) {  // (uniform: the timed launch only)
+  if (b.kt_stage == 2 && !g.merge_cap) {  // (uniform: the timed launch only)
     __syncthreads();
     if (t == 0) kt_end(b, 2);
   }
@@ -790,6 +881,7 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   const int f = blockIdx.y;
+  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + fo;
@@ -814,6 +906,7 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
 // one CCL tile got theirs from k_thr_ccl already and are not listed.)
 __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
   const int f = blockIdx.y;
+  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + fo;
@@ -824,6 +917,246 @@ __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
     const uint32_t l = lr[k];
     const uint32_t r = par[l];
     par[l] = r | (size[r] >= 25 ? kKeptBit : 0u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4+K5 in one workgroup per frame (throughput mode): the cross-tile merge of
+// the CCL (the reference's Merge across tiles and FinalLabeling's roots,
+// labeling_allegretti_2019_BKE.cu:302-462) on the frame's listed local roots --
+// the tile-local roots of components that reach a tile border, ~40 per tile --
+// held in LDS.  Each listed root is a union-find node keyed (gid << 32 | slot):
+// linking to the smaller key links to the smaller node id, so a component's root
+// is its minimum node id, the reference's label.  The unions are k_ccl_border's
+// candidate links (the same tests on the threshold plane); a node's slot is two
+// hops away (node -> local root, whose word k_thr_ccl set to kListBit | list
+// slot).  Then every listed root's word becomes root | kept (>= 25 pixels) and
+// the root's count its component's size: what k_ccl_roots + k_ccl_keep leave.
+// A frame with more listed roots than the LDS holds is handed back to those
+// kernels (words restored, ccl_ovf set).
+// ---------------------------------------------------------------------------
+constexpr int kMergePer = (kMergeCapMax + 1023) / 1024;  // listed roots per thread
+constexpr int kMergeItems = 2;                          // border blocks per thread per pass
+
+// (keys change under other threads' atomics: every read is a relaxed atomic load,
+// which the compiler may not reuse across iterations)
+__device__ __forceinline__ uint64_t key_load(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t merge_find(uint64_t* key, uint32_t i) {
+  uint64_t p = key_load(key + i);
+  while ((uint32_t)p != i) {
+    const uint64_t gp = key_load(key + (uint32_t)p);
+    if ((uint32_t)gp != (uint32_t)p) atomicMin((unsigned long long*)&key[i], (unsigned long long)gp);  // halving
+    i = (uint32_t)p;
+    p = gp;
+  }
+  return i;
+}
+
+__device__ __forceinline__ void merge_union(uint64_t* key, uint32_t a, uint32_t c) {
+  while (true) {
+    a = merge_find(key, a);
+    c = merge_find(key, c);
+    if (a == c) return;
+    const uint64_t ka = key_load(key + a), kc = key_load(key + c);  // roots: their own (gid << 32 | slot)
+    // linked meanwhile (a key names its slot only while it is a root): find again;
+    // a link succeeds only over the root's own key
+    if ((uint32_t)ka != a || (uint32_t)kc != c) continue;
+    if (ka < kc) {
+      const uint64_t old = atomicMin((unsigned long long*)&key[c], (unsigned long long)ka);
+      if (old == kc) return;
+      c = (uint32_t)old;  // c was linked meanwhile: join a with its new parent
+    } else {
+      const uint64_t old = atomicMin((unsigned long long*)&key[a], (unsigned long long)kc);
+      if (old == ka) return;
+      a = (uint32_t)old;
+    }
+  }
+}
+
+template <int TWD>
+__global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params prm) {
+  using CT = CclTile<TWD>;
+  constexpr int kBW = CT::BW, kBH = CT::BH;
+  constexpr int kNB = kBW + kBH + (kBH - 1);  // border blocks with candidate links: top row, left, right column
+  extern __shared__ uint64_t s_key[];          // [merge_cap] parent key (gid << 32 | slot)
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_key + g.merge_cap);  // [merge_cap] pixel counts
+  uint16_t* s_tile = reinterpret_cast<uint16_t*>(s_cnt + g.merge_cap);  // [merge_cap] tile of each slot
+  __shared__ uint32_t s_base[kMaxCclTiles + 1];
+  __shared__ uint32_t s_wsum[16];
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  kt_begin(b, 2);
+  // AT_PHASE_PROBE: frame 0's phase clocks in probe[40 + k]
+  auto stamp = [&](int k) {
+    if (AT_PROBE_ON(prm) && f == 0 && tid == 0) b.probe[40 + k] = wall_clock64();
+  };
+  stamp(0);
+  const int ntl = g.CTX * g.CTY;
+  const size_t fo = (size_t)f * g.Wd * g.Hd;
+  uint32_t* par = b.par + fo;
+  uint32_t* size = b.size + fo;
+  const uint8_t* thr = b.thr + fo;
+  const uint32_t* lroot = b.lroot + (size_t)f * ntl * kCclTileNodesMax;
+  // (0) list sizes -> slot bases, and the tile of every slot
+  const uint32_t nt = tid < ntl ? b.nlroot[(size_t)f * ntl + tid] : 0u;
+  uint32_t total = 0;
+  const uint32_t incl = block_incl_scan(nt, s_wsum, &total, 16);
+  if (tid < ntl) s_base[tid] = incl - nt;
+  if (tid == 0) {
+    s_base[ntl] = total;
+    b.nlr_tot[f] = total;
+  }
+  const bool fits = total <= (uint32_t)g.merge_cap;
+  __syncthreads();  // s_base complete
+  if (fits)
+    for (int t = tid >> 6; t < ntl; t += 16) {  // a wave per tile
+      const uint32_t b0 = s_base[t], n = s_base[t + 1] - b0;
+      for (uint32_t k = lane_id(); k < n; k += 64) s_tile[b0 + k] = (uint16_t)t;
+    }
+  __syncthreads();
+  if (!fits) {
+    // too many for the LDS: plain root words back, the multi-workgroup kernels merge it
+    for (int t = tid >> 6; t < ntl; t += 16) {
+      const uint32_t n = s_base[t + 1] - s_base[t];
+      for (uint32_t k = lane_id(); k < n; k += 64) {
+        const uint32_t l = lroot[(size_t)t * kCclTileNodesMax + k];
+        par[l] = l;
+      }
+    }
+    if (tid == 0) b.ccl_ovf[f] = 1u;
+    if (tid == 0) kt_end(b, 2);
+    return;
+  }
+  stamp(1);
+  // (1) the listed roots: node id and local pixel count (k_thr_ccl's lists)
+  const uint32_t* lcnt = b.lcnt + (size_t)f * ntl * kCclTileNodesMax;
+  uint32_t mg[kMergePer];
+#pragma unroll
+  for (int j = 0; j < kMergePer; j++) {
+    const uint32_t i = tid + 1024u * j;
+    mg[j] = 0;
+    if (i < total) {
+      const int t = s_tile[i];
+      const size_t e = (size_t)t * kCclTileNodesMax + (i - s_base[t]);
+      mg[j] = lroot[e];
+      s_cnt[i] = lcnt[e];
+      s_key[i] = ((uint64_t)mg[j] << 32) | i;
+    }
+  }
+  __syncthreads();
+  stamp(2);
+  // (2) the cross-tile links: k_ccl_border's tests on the tiles' border descriptors
+  // (CclDesc), items ordered by role so a wave's lanes read neighbouring entries:
+  // the top-row blocks of every tile (role 0, vs the tile above), the left-column
+  // blocks (role 1, vs the tile to the left), the right-column blocks of rows >= 1
+  // (role 2, the up-right diagonal into the tile to the right).  A lane skips a
+  // union equal to its left neighbour's (runs along a border link the same pair).
+  const uint32_t* desc = b.cdesc + (size_t)f * ntl * CclDesc::kWords;
+  auto dbyte = [&](int t, int w, int i) -> uint32_t {  // byte i of the u32 array at word w of tile t
+    return (uint32_t)reinterpret_cast<const uint8_t*>(desc + (size_t)t * CclDesc::kWords + w)[i];
+  };
+  auto dslot = [&](int t, int w, int i) -> uint32_t {
+    return (uint32_t)reinterpret_cast<const uint16_t*>(desc + (size_t)t * CclDesc::kWords + w)[i];
+  };
+  const int n0 = ntl * kBW, n1 = n0 + ntl * kBH, nitems = n1 + ntl * (kBH - 1);
+  for (int j0 = 0; j0 < nitems; j0 += 1024 * kMergeItems) {
+    uint32_t su[kMergeItems][5], sv[kMergeItems][5];  // slot pair per link (0xffffffff: none)
+#pragma unroll
+    for (int q = 0; q < kMergeItems; q++) {
+#pragma unroll
+      for (int k = 0; k < 5; k++) su[q][k] = sv[q][k] = 0xffffffffu;
+      const int j = j0 + tid + 1024 * q;
+      if (j >= nitems) continue;
+      if (j < n0) {  // top-row block x of tile t vs the bottom row of the tile above
+        const int t = j / kBW, x = j % kBW, ty = t / g.CTX, tx = t % g.CTX;
+        if (ty == 0 || tx * kBW + x >= g.BW) continue;
+        const int ta = t - g.CTX;
+        const bool hl = tx > 0, hr = tx + 1 < g.CTX;
+        const uint32_t a = dbyte(t, CclDesc::Tthr, 2 * x), bb = dbyte(t, CclDesc::Tthr, 2 * x + 1);
+        const uint32_t ul = x > 0 ? dbyte(ta, CclDesc::Bthr, 2 * x - 1) : (hl ? dbyte(ta - 1, CclDesc::Bthr, 2 * kBW - 1) : 127u);
+        const uint32_t u0 = dbyte(ta, CclDesc::Bthr, 2 * x), u1 = dbyte(ta, CclDesc::Bthr, 2 * x + 1);
+        const uint32_t ur = x + 1 < kBW ? dbyte(ta, CclDesc::Bthr, 2 * x + 2) : (hr ? dbyte(ta + 1, CclDesc::Bthr, 0) : 127u);
+        const uint32_t bF = s_base[t], bA = s_base[ta];
+        const uint32_t oF = dslot(t, CclDesc::TsF, x), oL = dslot(t, CclDesc::TsL, x), oR = dslot(t, CclDesc::TsR, x);
+        if (a == 255 && ul == 255) {  // P: up-left
+          const int tv = x > 0 ? ta : ta - 1;
+          su[q][0] = bF + oF;
+          sv[q][0] = s_base[tv] + dslot(tv, CclDesc::BsF, x > 0 ? x - 1 : kBW - 1);
+        }
+        if ((a == 255 || bb == 255) && (u0 == 255 || u1 == 255)) {  // Q: up
+          su[q][1] = bF + oF;
+          sv[q][1] = bA + dslot(ta, CclDesc::BsF, x);
+        }
+        if (bb == 255 && ur == 255) {  // R: up-right
+          const int tv = x + 1 < kBW ? ta : ta + 1;
+          su[q][2] = bF + oF;
+          sv[q][2] = s_base[tv] + dslot(tv, CclDesc::BsF, x + 1 < kBW ? x + 1 : 0);
+        }
+        if (a == 0 && u0 == 0) { su[q][3] = bF + oL; sv[q][3] = bA + dslot(ta, CclDesc::BsL, x); }  // bg up (left column)
+        if (bb == 0 && u1 == 0) { su[q][4] = bF + oR; sv[q][4] = bA + dslot(ta, CclDesc::BsR, x); }  // bg up (right)
+      } else if (j < n1) {  // left-column block y of tile t vs the right column of the tile to the left
+        const int t = (j - n0) / kBH, y = (j - n0) % kBH, ty = t / g.CTX, tx = t % g.CTX;
+        if (tx == 0 || ty * kBH + y >= g.BH) continue;
+        const int tl = t - 1;
+        const uint32_t a = dbyte(t, CclDesc::Lthr, 2 * y), c = dbyte(t, CclDesc::Lthr, 2 * y + 1);
+        const uint32_t ul = y > 0 ? dbyte(tl, CclDesc::Rthr, 2 * y - 1) : 127u;
+        const uint32_t l0 = dbyte(tl, CclDesc::Rthr, 2 * y), l1 = dbyte(tl, CclDesc::Rthr, 2 * y + 1);
+        const uint32_t bF = s_base[t], bL = s_base[tl];
+        const uint32_t oF = dslot(t, CclDesc::LsF, y), oL = dslot(t, CclDesc::LsL, y);
+        if (y > 0 && a == 255 && ul == 255) { su[q][0] = bF + oF; sv[q][0] = bL + dslot(tl, CclDesc::RsF, y - 1); }
+        if ((a == 255 || c == 255) && (l0 == 255 || l1 == 255)) { su[q][1] = bF + oF; sv[q][1] = bL + dslot(tl, CclDesc::RsF, y); }
+        if ((a == 0 && l0 == 0) || (c == 0 && l1 == 0)) { su[q][2] = bF + oL; sv[q][2] = bL + dslot(tl, CclDesc::RsR, y); }
+      } else {  // right-column block y >= 1 of tile t: up-right into the tile to the right
+        const int t = (j - n1) / (kBH - 1), y = 1 + (j - n1) % (kBH - 1), ty = t / g.CTX, tx = t % g.CTX;
+        if ((tx + 1) * kBW > g.BW || ty * kBH + y >= g.BH || tx + 1 >= g.CTX) continue;
+        const uint32_t bb = dbyte(t, CclDesc::Rthr, 2 * y), ur = dbyte(t + 1, CclDesc::Lthr, 2 * y - 1);
+        if (bb == 255 && ur == 255) {
+          su[q][0] = s_base[t] + dslot(t, CclDesc::RsF, y);
+          sv[q][0] = s_base[t + 1] + dslot(t + 1, CclDesc::LsF, y - 1);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kMergeItems; q++)
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const bool on = su[q][k] != 0xffffffffu && sv[q][k] < (uint32_t)total && su[q][k] < (uint32_t)total;
+        const uint32_t pair = on ? (su[q][k] << 16 | sv[q][k]) : 0xffffffffu;
+        const uint32_t prev = wave_shr1(pair, 0xfffffffeu);
+        if (on && pair != prev) merge_union(s_key, su[q][k], sv[q][k]);
+      }
+  }
+  __syncthreads();
+  stamp(3);
+  // (3) component sizes at the roots
+#pragma unroll
+  for (int j = 0; j < kMergePer; j++) {
+    const uint32_t i = tid + 1024u * j;
+    if (i < total) {
+      const uint32_t r = merge_find(s_key, i);
+      if (r != i) atomicAdd(&s_cnt[r], s_cnt[i]);
+    }
+  }
+  __syncthreads();
+  stamp(4);
+  // (4) every listed root's word: root | kept; the root's count: its component's size
+#pragma unroll
+  for (int j = 0; j < kMergePer; j++) {
+    const uint32_t i = tid + 1024u * j;
+    if (i < total) {
+      const uint32_t r = merge_find(s_key, i);  // (one hop after (3)'s halving, mostly)
+      const uint32_t n = s_cnt[r];
+      const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
+      par[mg[j]] = root | (n >= 25 ? kKeptBit : 0u);
+      if (r == i) size[mg[j]] = n;
+    }
+  }
+  stamp(5);
+  if (b.kt_stage == 2) {  // (uniform: the timed launch only)
+    __syncthreads();
+    if (tid == 0) kt_end(b, 2);
   }
 }
 
@@ -851,11 +1184,6 @@ __device__ uint32_t ht_slot_find(const uint64_t* keys, uint64_t key) {
   return 0xffffffffu;
 }
 
-// Value of lane l-1 in lane l (lane 0: `fill`): one DPP wave_shr:1 move per
-// dword instead of a ds_bpermute round trip through LDS.
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
-}
 __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) {
   return (uint64_t)wave_shr1((uint32_t)v, 0) | ((uint64_t)wave_shr1((uint32_t)(v >> 32), 0) << 32);
 }
@@ -3347,7 +3675,17 @@ template <int NT, int CAP, bool FUSE = false>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
-  if (!nlo) kt_begin(b, 9);  // (the device-clock span times the first launch)
+  // device-clock span: the first launch's workgroups stamp their slots as usual; the
+  // second (nlo != 0) appends its stamps after them (a slot per workgroup claimed on
+  // the grid counter the first launch set), so the span covers both launches, as
+  // the HIP events around the stage do
+  uint32_t kt_slot = ~0u;
+  if (!nlo) {
+    kt_begin(b, 9);
+  } else if (b.kt_stage == 9 && tid == 0) {
+    kt_slot = atomicAdd(b.kgrid, 1u);
+    if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
+  }
   uint32_t* pacc = S.pacc;
   if (tid < 22) pacc[tid] = 0;
   if (tid == 0) S.slow_dt = 0;
@@ -3380,6 +3718,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
   if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
   if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
   if (tid == 0 && !nlo) kt_end(b, 9);
+  if (tid == 0 && nlo && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
@@ -4284,6 +4623,15 @@ hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bg
   return hipGetLastError();
 }
 
+static size_t merge_lds_bytes(const Geom& g) { return (size_t)g.merge_cap * 14; }
+
+// one-time kernel attributes: k_ccl_merge's dynamic LDS beyond the default limit
+hipError_t prepare_kernels(const Geom& g) {
+  if (!g.merge_cap) return hipSuccess;
+  return hipFuncSetAttribute((const void*)k_ccl_merge<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)merge_lds_bytes(g));
+}
+
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,
                            hipStream_t st, hipEvent_t* ev, hipStream_t st2, hipEvent_t fork, hipEvent_t join,
                            const KernelTimer* kt) {
@@ -4331,8 +4679,12 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(2, st, 0);
     if (!on(2)) {}
     else if (g.ctw == 32) hipLaunchKernelGGL(k_ccl_border<32>, grd, dim3(BorderRoles<32>::NT), 0, st, b, g);
+    else if (g.merge_cap) hipLaunchKernelGGL(k_ccl_merge<64>, dim3(B), dim3(1024), merge_lds_bytes(g), st, b, g, prm);
     else hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
     tk(2, st, 1);
+    // frames k_ccl_merge could not hold: the multi-workgroup merge (the others exit at once)
+    if (on(2) && g.ctw != 32 && g.merge_cap)
+      hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
     mark();
   }
   tk(3, st, 0);

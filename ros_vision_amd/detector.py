@@ -441,12 +441,13 @@ class GpuDetector:
         return ms.value, n.value
 
     BATCH_STATS = ("frames", "boundary_points", "pairs", "small_blob_points", "large_blob_points",
-                   "quads", "candidates", "host_wait_us_total", "host_tail_us_total")
+                   "quads", "candidates", "host_wait_us_total", "host_tail_us_total", "ccl_listed_roots",
+                   "ccl_listed_roots_max", "ccl_fallback_frames")
 
     def batch_stats(self):
         """Work counts of the last collected batch (see at_batch_stats)."""
-        buf = (C.c_uint64 * 9)()
-        n = _check(load_library().at_batch_stats(self._h, buf, 9), "at_batch_stats")
+        buf = (C.c_uint64 * len(self.BATCH_STATS))()
+        n = _check(load_library().at_batch_stats(self._h, buf, len(buf)), "at_batch_stats")
         return dict(zip(self.BATCH_STATS, [int(x) for x in buf[:n]]))
 
     def detections(self, frame=0):

@@ -456,3 +456,28 @@ def test_dense_frames_keep_every_candidate(gpu, oracle_mod, batch):
         if c < 3:
             assert len(res[c]) > 128
         assert len(det.poses(c)) == len(res[c])
+
+
+def test_ccl_merge_and_fallback_in_one_batch(gpu, oracle_mod):
+    """Throughput mode merges each frame's listed local roots in one workgroup's LDS
+    (k_ccl_merge); a frame with more (white noise: thousands of tile-border specks)
+    goes to the multi-workgroup kernels (k_ccl_border / k_ccl_roots / k_ccl_keep).
+    Both kinds of frame in one batch: every stage bit-exact against the oracle
+    (labels = the component's minimum node id, labeling_allegretti_2019_BKE.cu:340-462)."""
+    from ros_vision_amd import synth
+    rng = np.random.default_rng(99)
+    yy, xx = np.mgrid[0:720, 0:1280]
+    frames = [synth.stream_frame(1280, 720, 9)[1],
+              rng.integers(0, 256, size=(720, 1280), dtype=np.uint8),
+              synth.stream_frame(1280, 720, 10)[1],
+              # a one-decimated-pixel checker: every border block its own background specks
+              np.where(((xx // 2) + (yy // 2)) & 1, 230, 25).astype(np.uint8)]
+    det = gpu.GpuDetector(1280, 720, max_batch=8)
+    res = det.detect_batch(frames, gpu.AT_FMT_GRAY8)
+    st = det.batch_stats()
+    assert st["ccl_fallback_frames"] >= 1 and st["ccl_fallback_frames"] < len(frames), st
+    for c, f in enumerate(frames):
+        orc = oracle_mod.Oracle(1280, 720)
+        orc.detect(f, 2)
+        assert compare_frame(det, orc, frame_idx=c) == [], c
+        assert compare_detections(res[c], orc.detections()) == [], c

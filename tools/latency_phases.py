@@ -35,6 +35,12 @@ for name, idx in (("small", 200), ("large", 201)):
     print("slowest %s item: %.2f us, %d points" % (name, (v >> 20) / 100.0, v & 0xfffff))
 nbig = max(1, int(p[220]))
 print("large blobs > 2048 points (%d): mean phase us" % int(p[220]), [round(p[208 + k] / 100.0 / nbig, 2) for k in range(10)])
+if B >= 8 and p[63]:
+    nw = float(p[63])
+    print("k_thr_ccl phases (us per workgroup, %d workgroups): loads %.2f  filter %.2f  threshold %.2f  runs %.2f  targets %.2f  "
+          "unions %.2f  finds %.2f  counts %.2f  publish %.2f" % ((int(nw),) + tuple(p[48 + k] / nw / 100.0 for k in range(9))))
+if B >= 8:
+    print("k_ccl_merge phases (us, frame 0): base %.2f  roots %.2f  links %.2f  sizes %.2f  words %.2f" % tuple(np.diff(p[40:46]) / 100.0))
 print("k_pairs phases (us): merge %.2f  list %.2f  rank %.2f  scan %.2f  work+bases %.2f" % tuple(np.diff(p[0:6]) / 100.0))
 print("pose phases (us): polar3 %.2f  OI-1 %.2f  ambiguity %.2f  OI-2 %.2f" % tuple(np.diff(p[16:21]) / 100.0))
 a = p[16 + 2]
