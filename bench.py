@@ -33,6 +33,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec + p50 per-frame latency, 1280x720 AprilTag detect at 1/2/4/8 MI355X"
+# The roofline's kernel, by a fixed rule rather than by the stage profile of the box
+# (the top serialized stages are within ~10 % of each other and swapped places
+# between boxes): the kernel with the largest marginal cost in the concurrent bench
+# loop -- throughput with the sequence cut after each stage (tools/ablate.sh,
+# profiles/r04c/ablation.txt: k_thr_ccl 0.235 ms of 1.23 ms per step, then
+# k_boundary 0.222, k_blob_small 0.185).
+DOMINANT = "k_thr_ccl"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -92,10 +99,13 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_extents":  # candidate points read (bounded by all boundary points), kept points' keys written
         return 8 * stats.get("boundary_points", 0) + 8 * (stats.get("small_blob_points", 0) +
                                                           stats.get("large_blob_points", 0))
-    if kernel == "k_thr_ccl":
-        return nf * 9 * Wd * Hd                            # dec in; thr, parents, sizes out
+    if kernel == "k_thr_ccl":  # dec in; thr and parent words out; lists (id, count) and border descriptors out
+        tiles = ((Wd + 63) // 64) * ((Hd + 31) // 32)
+        return nf * 6 * Wd * Hd + 8 * stats.get("ccl_listed_roots", 0) + nf * tiles * 704
     if kernel == "k_ccl_border":  # per 32x32 tile: 47 border blocks, thr bytes + parent words
         return nf * ((Wd + 31) // 32) * ((Hd + 31) // 32) * 47 * 16
+    if kernel == "k_ccl_merge":  # border descriptors (704 B per 64x32 tile) + listed roots (id, count) in, words out
+        return nf * ((Wd + 63) // 64) * ((Hd + 31) // 32) * 704 + 12 * stats.get("ccl_listed_roots", 0)
     if kernel == "k_pose":  # per candidate detection: H + corners in, R, t, errors out
         return stats.get("candidates", 0) * (72 + 64 + 112)
     return None
@@ -213,25 +223,22 @@ def main():
         ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
         rec_cap = 32  # detection records per frame gathered to rank 0 (fixed capacity)
         rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)
-        send = [torch.empty((B, rec_bytes + 4), dtype=torch.uint8, device="cuda") for _ in range(2)]
-        recv = ([[torch.empty_like(send[0]) for _ in range(world)] for _ in range(2)] if rank == 0 else [None, None])
-        cnt_host = [torch.empty((B,), dtype=torch.int32).pin_memory() for _ in range(2)]
-        copied = {}  # detector -> event after the async copies out of its pinned buffer
-        gwork = [None, None]
+        copied = {}  # detector -> event after the async copy out of its pinned buffer
+        gather = multigpu.RecordGather(dist, B, rec_bytes, "cuda")
 
     def gather_results(d, s):
-        """Fixed-capacity detection records of this rank's batch -> rank 0 (RCCL gather).
-        at_collect wrote them into pinned host memory: one async copy each, no staging."""
-        i = s % 2
-        if gwork[i] is not None:
-            gwork[i].wait()
-        recs = d._out_t.view(B, -1)[:, :rec_bytes]
-        send[i][:, 4:].copy_(recs, non_blocking=True)
-        cnt_host[i].copy_(torch.tensor([min(d._n[f], rec_cap) for f in range(B)], dtype=torch.int32))
-        send[i][:, :4].copy_(cnt_host[i].view(torch.uint8).view(B, 4), non_blocking=True)
-        copied[id(d)] = torch.cuda.Event()
-        copied[id(d)].record()
-        gwork[i] = dist.gather(send[i], gather_list=recv[i], dst=0, async_op=True)
+        """Fixed-capacity detection records of the other ranks' batches -> rank 0
+        (multigpu.RecordGather: RCCL point-to-point).  at_collect wrote them into
+        pinned host memory, read by an async copy; rank 0's own stay there, at world
+        size 1 nothing moves."""
+        if world == 1:
+            return
+        if rank == 0:
+            gather.post(s)
+        else:
+            gather.post(s, d._out_t.view(B, -1)[:, :rec_bytes],
+                        torch.tensor([min(d._n[f], rec_cap) for f in range(B)], dtype=torch.int32))
+            copied[id(d)] = gather.copied[s % 2]
 
     runner = StreamRunner(dets, base, stride, npool, B)
 
@@ -274,9 +281,8 @@ def main():
                 ingest.start(s + 1)  # its buffer was read by step s+1-instances, collected above
         while inflight:
             ndet += drain()
-        for w in gwork:
-            if w is not None:
-                w.wait()
+        gather.drain()
+        ingest.drain()
         return ndet
 
     run(max(1, args.warmup))
@@ -292,7 +298,7 @@ def main():
             prof.collect()
         stages, stage_batches = prof.stage_times()
         prof.set_profiling(False)
-    dominant = args.timed_kernel or (max(stages, key=stages.get) if stages else "k_blob")
+    dominant = args.timed_kernel or DOMINANT
     # live per-launch time of the dominant kernel inside the timed region
     ktimer = None if args.no_kernel_timer else dominant
     for d in dets:
@@ -412,6 +418,16 @@ def main():
             k_traffic = round(B * sum(2 * v["fetch_bytes_per_frame"] + v["write_bytes_per_frame"] for v in kk))
     k_achieved = kbytes / (k_ms * 1e-3) / 1e9 if (kbytes and k_ms > 0) else None
     pipe_bytes = 3 * W * H  # read YUYV 2WH + write gray WH
+    # the three largest serialized stages on their own (stage profile: HIP events
+    # between the kernels of one batch in flight): algorithmic bytes / stage time
+    isolated = []
+    for kname in sorted(stages, key=stages.get, reverse=True)[:3]:
+        kb = kernel_algorithmic_bytes(kname, stats, W, H)
+        ms = stages[kname]
+        gbs = kb / (ms * 1e-3) / 1e9 if (kb and ms > 0) else None
+        isolated.append({"kernel": kname, "ms_per_batch": round(ms, 4), "algorithmic_bytes_per_launch": kb,
+                         "achieved": round(gbs, 3) if gbs else None,
+                         "frac": round(gbs / HBM_PEAK_GBS, 6) if gbs else None})
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -455,7 +471,9 @@ def main():
                      "avg_launch_ms_hip_events": round(k_ms_events, 5),
                      "frac_hip_events": round(kbytes / (k_ms_events * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
                      if (kbytes and k_ms_events > 0) else None,
-                     "note": "dominant kernel by stage time, timed in the timed region on every launch: "
+                     "isolated_top3": isolated,
+                     "note": "kernel named by a fixed rule (DOMINANT: the largest marginal cost in the concurrent "
+                             "loop, profiles/r04c/ablation.txt), timed in the timed region on every launch: "
                              "avg_launch_ms = its execution span on the device wall clock (first workgroup "
                              "start to last workgroup end, at_kernel_span; what rocprofv3 --kernel-trace "
                              "reports), avg_launch_ms_hip_events = HIP events around it on its stream (adds "

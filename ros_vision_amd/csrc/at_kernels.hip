@@ -713,31 +713,36 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     // scattered threshold bytes and parent words
     const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
     uint32_t* dw = b.cdesc + tl * CclDesc::kWords;
-    uint16_t* dh = reinterpret_cast<uint16_t*>(dw);
-    auto slot = [&](uint32_t n, uint32_t r) -> uint16_t { return n ? s_li[r] : (uint16_t)0xffffu; };
-    if (bty == 0) {
-      dh[2 * CclDesc::TsF + btx] = slot(nfg, rF);
-      dh[2 * CclDesc::TsL + btx] = slot(nbl, rL);
-      dh[2 * CclDesc::TsR + btx] = slot(nbr, rR);
+    // whole-word stores: a wave holds two block rows, so the slots of blocks (x, x+1)
+    // of a row are in lanes l, l+1 and those of block rows (2i, 2i+1) of a column in
+    // lanes l, l+32 of wave i
+    if (!(AT_TC_EXP & 8)) {
+    const uint32_t sF = nfg ? s_li[rF] : 0xffffu, sL = nbl ? s_li[rL] : 0xffffu, sR = nbr ? s_li[rR] : 0xffffu;
+    const uint32_t nF = wave_read_next(sF), nL = wave_read_next(sL), nR = wave_read_next(sR);
+    const int w = tid >> 6;
+    if ((bty == 0 || bty == CT::BH - 1) && !(btx & 1)) {
+      const int o = bty == 0 ? 0 : CclDesc::BsF - CclDesc::TsF;
+      dw[CclDesc::TsF + o + (btx >> 1)] = sF | (nF << 16);
+      dw[CclDesc::TsL + o + (btx >> 1)] = sL | (nL << 16);
+      dw[CclDesc::TsR + o + (btx >> 1)] = sR | (nR << 16);
     }
-    if (bty == CT::BH - 1) {
-      dh[2 * CclDesc::BsF + btx] = slot(nfg, rF);
-      dh[2 * CclDesc::BsL + btx] = slot(nbl, rL);
-      dh[2 * CclDesc::BsR + btx] = slot(nbr, rR);
+    const uint32_t dF = __shfl(sF, (int)(lane & 31) + 32), dL = __shfl(sL, (int)(lane & 31) + 32),
+                   dR = __shfl(sR, (int)(lane & 31) + 32);
+    if (lane == 0) {
+      dw[CclDesc::LsF + w] = sF | (dF << 16);
+      dw[CclDesc::LsL + w] = sL | (dL << 16);
     }
-    if (btx == 0) {
-      dh[2 * CclDesc::LsF + bty] = slot(nfg, rF);
-      dh[2 * CclDesc::LsL + bty] = slot(nbl, rL);
+    if (lane == kCclBW - 1) {
+      dw[CclDesc::RsF + w] = sF | (dF << 16);
+      dw[CclDesc::RsR + w] = sR | (dR << 16);
     }
-    if (btx == kCclBW - 1) {
-      dh[2 * CclDesc::RsF + bty] = slot(nfg, rF);
-      dh[2 * CclDesc::RsR + bty] = slot(nbr, rR);
     }
     // threshold bytes (127 outside the image): rows 0 and 31, columns 0 and 63
     auto row4 = [&](int r, int c) -> uint32_t {  // (byte reads: the rows start at odd offsets)
       return s_t[r][c] | (s_t[r][c + 1] << 8) | (s_t[r][c + 2] << 16) | ((uint32_t)s_t[r][c + 3] << 24);
     };
-    if (tid < 16) {
+    if (AT_TC_EXP & 16) {
+    } else if (tid < 16) {
       dw[CclDesc::Tthr + tid] = row4(1, 1 + 4 * tid);
     } else if (tid < 32) {
       dw[CclDesc::Bthr + tid - 16] = row4(kCclTileH, 1 + 4 * (tid - 16));
@@ -1880,20 +1885,37 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
     __syncthreads();
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(pts);
-    auto place = [&](uint32_t w) {
+    // called by every lane of the wave (valid: the lane holds a point): lanes in a
+    // run of equal entries (points come in emission order, mostly one pair after
+    // another) reserve their slots with ONE LDS atomic by the run's head
+    const uint32_t lane = lane_id();
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    auto place = [&](uint32_t w, bool valid) {
       const uint32_t e = w >> 23;
-      const uint32_t base = e < (uint32_t)kGrpEnt ? s_base[e] : kGrpFallback;
-      if (base == kGrpDrop) return;
-      if (base != kGrpFallback) grp[base + atomicAdd(&s_cur[e], 1u)] = narrow_bits(w);
-      else place_global(b.pent_key[tb * kLdsPairSlots + e], narrow_bits(w));
+      const uint32_t base = (valid && e < (uint32_t)kGrpEnt) ? s_base[e] : kGrpFallback;
+      const bool lds = valid && base != kGrpFallback && base != kGrpDrop;
+      const uint32_t key = lds ? e : 0x80000000u + lane;  // (never equal to a neighbour's)
+      const bool same = lds && wave_shr1(key, 0xffffffffu) == key;
+      const uint64_t same_mask = __ballot(same);
+      const bool head = lds && !same;
+      uint32_t start = 0;
+      if (head) start = atomicAdd(&s_cur[e], run_len(same_mask, lane));
+      const uint64_t heads = __ballot(head);
+      const int hl = (heads & le) ? 63 - __builtin_clzll(heads & le) : (int)lane;
+      const uint32_t s0 = (uint32_t)__shfl((int)start, hl);
+      if (lds) grp[base + s0 + (lane - (uint32_t)hl)] = narrow_bits(w);
+      else if (valid && base == kGrpFallback) place_global(b.pent_key[tb * kLdsPairSlots + e], narrow_bits(w));
     };
 #pragma unroll
     for (int k = 0; k < kGrpPre; k++) {
       const uint32_t i = 2 * (tid + 256 * k);
-      if (i < n) place((uint32_t)pv[k]);
-      if (i + 1 < n) place((uint32_t)(pv[k] >> 32));
+      place((uint32_t)pv[k], i < n);
+      place((uint32_t)(pv[k] >> 32), i + 1 < n);
     }
-    for (uint32_t i = tid + 512 * kGrpPre; i < n; i += 256) place(pw[i]);
+    for (uint32_t i0 = 512 * kGrpPre; i0 < n; i0 += 256) {
+      const uint32_t i = i0 + tid;
+      place(i < n ? pw[i] : 0u, i < n);
+    }
     return;
   }
   for (int i = tid; i < 2 * kGrpEnt; i += 256) s_hk[i] = 0;

@@ -139,3 +139,51 @@ def test_scatter_ingest_double_buffer_world2():
             off = (s * B) % npool
             want.append([16 * r + off + k for k in range(B)])
         assert res[r] == want
+
+
+def _gather_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from ros_vision_amd import multigpu
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, rb = 3, 8
+    g = multigpu.RecordGather(dist, B, rb, "cpu")
+    got = []
+    for s in range(5):  # step s: rank r's record bytes = 10*r + s, counts = r + s + frame
+        recs = torch.full((B, rb), 10 * rank + s, dtype=torch.uint8)
+        cnt = torch.tensor([rank + s + f for f in range(B)], dtype=torch.int32)
+        g.post(s, recs, cnt)
+        if s >= 1 and rank == 0:  # results of the previous step (double buffered)
+            res = g.result(s - 1)
+            got.append({r: (int(t[0, 4]), t[:, :4].contiguous().view(torch.int32).ravel().tolist()) for r, t in res.items()})
+    if rank == 0:
+        res = g.result(4)
+        got.append({r: (int(t[0, 4]), t[:, :4].contiguous().view(torch.int32).ravel().tolist()) for r, t in res.items()})
+    g.drain()
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_record_gather_world3():
+    """bench.py --ingest scatter: detection records of ranks 1..N-1 reach rank 0 by
+    point-to-point sends (rank 0's own never move), double-buffered over steps."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(res[0]) == 5
+    for s, step in enumerate(res[0]):
+        assert sorted(step) == [1, 2]
+        for r in (1, 2):
+            assert step[r] == (10 * r + s, [r + s + f for f in range(3)])
