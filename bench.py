@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--c3-latency-iters", type=int, default=300,
                     help="config C3 latency: one batch of 4 camera frames (pageable host memory) -> detections, "
                          "p50 over this many batches; 0 = skip")
+    ap.add_argument("--node-path-calls", type=int, default=300,
+                    help="the deployed node's per-frame path, B=1: DetectorCore::process on bgr8 host frames "
+                         "at 1920x1080 and 800x600 (node/at_mock_node --time), p50/p99 per call; 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
     ap.add_argument("--timed-kernel", default=None,
@@ -173,6 +176,40 @@ def cpu_baseline(frames, width, height):
                       "synthetic frames: %d frames single-thread for latency, %d threads x %d frames for "
                       "throughput (threads = affinity mask %d capped by the cgroup CPU quota %s)"
                       % (nf, lat_iters, r["threads"], thr_iters, affinity, quota)}
+
+
+def node_path_latency(calls):
+    """The path the ROS 2 node runs per image (apriltags_cuda_detector.cu:382-557, what
+    its measurement_mode CSV times): DetectorCore::process on a bgr8 host frame --
+    at_detect (the frame to HBM, BGR -> luma on the GPU, detection, poses), robot frame,
+    distance sort, TagDetectionArray / NetworkTables / ApriltagListProto payloads, and the
+    outlined image drawn on the GPU and copied out (at_annotate_staged) -- at the
+    deployed geometries of system_config.json (1920x1080; 800x600: 400x300 decimated,
+    partial tiles).  Runs node/at_mock_node (a child process) on 4 rendered frames."""
+    from ros_vision_amd import synth
+    exe = os.path.join(ROOT, "node", "at_mock_node")
+    if not os.path.exists(exe) or calls <= 0:
+        return None
+    out = {}
+    for (W, H, ntags) in ((1920, 1080, 24), (800, 600, 8)):
+        frames = []
+        for k in range(4):
+            g, _ = synth.render_board(W, H, seed=5150 + 7 * k + W, ntags=ntags, side_range=(48, 96))
+            frames.append(np.repeat(g[:, :, None], 3, axis=2))  # bgr8 (gray board in every channel)
+        fd, path = tempfile.mkstemp(prefix="node_frames_", suffix=".bgr")
+        os.close(fd)
+        try:
+            np.stack(frames).tofile(path)
+            r = subprocess.run([exe, "--width", str(W), "--height", str(H), "--format", "bgr8", "--frames", path,
+                                "--time", str(calls)], capture_output=True, text=True, timeout=300)
+            lines = [l for l in r.stdout.splitlines() if l.startswith('{"timing"')]
+            if r.returncode == 0 and lines:
+                out["%dx%d" % (W, H)] = json.loads(lines[-1])["timing"]
+            else:
+                out["%dx%d" % (W, H)] = {"error": (r.stderr or "no output")[-200:]}
+        finally:
+            os.unlink(path)
+    return out
 
 
 def main():
@@ -494,6 +531,11 @@ def main():
         "pipeline_gpu_ms_per_batch": round(pipe_ms, 4) if pipe_ms else None,
         "cpu_baseline": None,
     }
+    if world == 1 and args.node_path_calls > 0:
+        try:
+            out["node_path_latency"] = node_path_latency(args.node_path_calls)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["node_path_latency"] = {"error": str(e)[:200]}
     if world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(frames, W, H)

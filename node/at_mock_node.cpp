@@ -9,13 +9,18 @@
 //
 // usage: at_mock_node --camera-serial S --format bgr8|yuyv|gray --frames F [--count N]
 //        [--vision-config-dir D] [--pin-to-core C --priority P]
-//        [--measurement-csv PATH] [--proto-out P] [--image-out I] [--device K]
+//        [--measurement-csv PATH] [--proto-out P] [--image-out I] [--device K] [--time N]
 //   As the reference node (apriltags_cuda_detector.cu:137-193): the frame size, the
 //   intrinsics and the extrinsics come from the camera serial's records in the
 //   vision_config_data share directory, found through $AMENT_PREFIX_PATH
 //   (ament_index) or given with --vision-config-dir.  Without a serial's records
 //   (test setups) --width W --height H [--calibration-dir D] [--system-config C]
 //   give them directly (calibration default: the reference test camera).
+//   --time N: after one untimed pass, N calls of DetectorCore::process over the frames
+//   in turn (the whole callback: detect, poses, robot frame, messages, proto and, for
+//   bgr8, the outlined image drawn on the GPU and copied out), one JSON line with the
+//   p50 / p99 wall time per call instead of the per-frame lines.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -44,7 +49,7 @@ void on_camera(void* ctx, const std::vector<at_node::TagDetectionMsg>& v) { ((Si
 }  // namespace
 
 int main(int argc, char** argv) {
-  int W = 0, H = 0, count = -1, device = 0, pin = -1, priority = 80;
+  int W = 0, H = 0, count = -1, device = 0, pin = -1, priority = 80, time_n = 0;
   std::string fmt_s = "yuyv", frames_path, calib_dir, serial = "N/A", sys_cfg, csv, proto_out, image_out, share_dir;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -63,6 +68,7 @@ int main(int argc, char** argv) {
     else if (k == "--vision-config-dir") share_dir = v;
     else if (k == "--pin-to-core") pin = std::atoi(v.c_str());
     else if (k == "--priority") priority = std::atoi(v.c_str());
+    else if (k == "--time") time_n = std::atoi(v.c_str());
     else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
   }
   at_node::Params prm;
@@ -117,6 +123,33 @@ int main(int argc, char** argv) {
     core.ctx = &sink;
     at_node::FrameOutputs out;
     std::vector<uint8_t> image;
+    if (time_n > 0) {  // the node's per-frame path, timed
+      std::vector<double> ms, det_ms;
+      for (int it = -count; it < time_n; ++it) {  // (the first pass over the frames is warm-up)
+        const int f = ((it % count) + count) % count;
+        const double stamp = 1000.0 + 0.02 * (it + count);
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = core.process(all.data() + (size_t)f * fb, fmt, stamp, stamp, &out,
+                                    fmt == AT_FMT_BGR8 ? &image : nullptr);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc != AT_OK && rc != AT_E_CAPACITY) {
+          std::fprintf(stderr, "frame %d: %s\n", f, at_strerror(rc));
+          return 1;
+        }
+        if (it >= 0) {
+          ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+          det_ms.push_back(out.det_time_us * 1e-3);
+        }
+      }
+      auto pct = [](std::vector<double> v, double q) {
+        std::sort(v.begin(), v.end());
+        return v[std::min(v.size() - 1, (size_t)(q * (v.size() - 1) + 0.5))];
+      };
+      std::printf("{\"timing\":{\"calls\":%d,\"format\":\"%s\",\"width\":%d,\"height\":%d,\"p50_ms\":%.4f,"
+                  "\"p99_ms\":%.4f,\"p50_detect_ms\":%.4f,\"detections_last\":%zu}}\n",
+                  time_n, fmt_s.c_str(), W, H, pct(ms, 0.5), pct(ms, 0.99), pct(det_ms, 0.5), out.detections.size());
+      return 0;
+    }
     for (int f = 0; f < count; ++f) {
       const double stamp = 1000.0 + 0.02 * f;
       const int rc = core.process(all.data() + (size_t)f * fb, fmt, stamp, stamp, &out,

@@ -348,6 +348,13 @@ constexpr uint32_t kListBit = 0x40000000u;
 // (only those can take part in k_ccl_border's unions)
 constexpr uint32_t kTouchBit = 0x80000000u;
 
+// SGPR budget of k_thr_ccl: .sgpr_count <= 80 keeps 8 waves per SIMD (4 of its 8-wave
+// workgroups per CU); at 82 (the border descriptor's addressing) the CU holds 7 waves
+// per SIMD, i.e. 3 workgroups: k_thr_ccl 0.24 -> 0.30 ms per 128 frames
+// (MI355X_MICROARCH.md: admitted blocks = 800 / (ceil(sgpr / 16) * 16 + 16))
+#ifndef AT_THR_SGPRS
+#define AT_THR_SGPRS 80
+#endif
 #ifndef AT_TC_EXP
 #define AT_TC_EXP 0  // (cost attribution builds only)
 #endif
@@ -358,7 +365,7 @@ constexpr uint32_t kTouchBit = 0x80000000u;
 // 8-pixel halo its filtered tile min/max needs, so there is no min/max plane,
 // no re-read of the decimated plane and one launch less.
 template <int TWD, int PRE>
-__global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
+__global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT_THR_SGPRS))) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
   constexpr int NT = CT::NT;
   constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES, kCclRowNodes = CT::ROW_NODES;
@@ -649,7 +656,27 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
   ph(8);
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
-  if (BY < g.BH && BX < g.BW) {
+  const bool inimg = BY < g.BH && BX < g.BW;
+  // sizes only at local roots with pixels: every other entry is never read
+  // (k_boundary reads component roots, k_ccl_roots the listed local roots; the
+  // AT_STAGE_SIZES tap masks the plane with the forest, k_tap_sizes)
+  const uint32_t wF = inimg && rF == F ? s_cnt[F] : 0u, wL = inimg && rL == L ? s_cnt[L] : 0u,
+                 wR = inimg && rR == R ? s_cnt[R] : 0u;
+  const uint32_t cF = wF & ~kTouchBit, cL = wL & ~kTouchBit, cR = wR & ~kTouchBit;
+  // the tile's local roots of components reaching its border (with pixels), listed for
+  // the cross-tile merge (k_ccl_merge; k_ccl_border / k_ccl_roots / k_ccl_keep)
+  const bool lF = cF && (wF & kTouchBit), lL = cL && (wL & kTouchBit), lR = cR && (wR & kTouchBit);
+  const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
+                 iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
+  constexpr bool kKeep = TWD != 32;
+  if constexpr (kKeep && !(AT_TC_EXP & 4)) {  // list slots of the roots, for the border descriptor
+    if (lF) s_li[F] = (uint16_t)iF;
+    if (lL) s_li[L] = (uint16_t)iL;
+    if (lR) s_li[R] = (uint16_t)iR;
+    __syncthreads();  // (the descriptor below reads other threads' roots' slots)
+  }
+  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+  if (inimg) {
     auto gid = [&](uint32_t s) -> uint32_t {
       const int sty = s / kCclRowNodes, r = s % kCclRowNodes;
       const int gy = y0 / 2 + sty;
@@ -661,36 +688,18 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
     uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
     const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
     const uint32_t idL = idF + g.Wd;
-    // sizes only at local roots with pixels: every other entry is never read
-    // (k_boundary reads component roots, k_ccl_roots the listed local roots; the
-    // AT_STAGE_SIZES tap masks the plane with the forest, k_tap_sizes)
-    const uint32_t wF = rF == F ? s_cnt[F] : 0u, wL = rL == L ? s_cnt[L] : 0u, wR = rR == R ? s_cnt[R] : 0u;
-    const uint32_t cF = wF & ~kTouchBit, cL = wL & ~kTouchBit, cR = wR & ~kTouchBit;
     // a root of a tile-interior component is final: in throughput mode (k_ccl_keep
     // follows) its parent word gets the kept bit here and it is not listed
-    constexpr bool kKeep = TWD != 32;
     auto fin = [&](uint32_t w, uint32_t c) -> uint32_t {
       return (kKeep && c && !(w & kTouchBit) && c >= 25) ? kKeptBit : 0u;
     };
-    // the tile's local roots of components reaching its border (with pixels), for
-    // the cross-tile merge (k_ccl_merge; k_ccl_border / k_ccl_roots / k_ccl_keep)
-    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
     uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-    const bool lF = cF && (wF & kTouchBit), lL = cL && (wL & kTouchBit), lR = cR && (wR & kTouchBit);
-    const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
-                   iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
     uint32_t* lc = b.lcnt + tl * kCclTileNodesMax;
     if (lF) { lr[iF] = gid(F); if (!(AT_TC_EXP & 2)) lc[iF] = cF; }
     if (lL) { lr[iL] = gid(L); if (!(AT_TC_EXP & 2)) lc[iL] = cL; }
     if (lR) { lr[iR] = gid(R); if (!(AT_TC_EXP & 2)) lc[iR] = cR; }
-    if constexpr (kKeep && !(AT_TC_EXP & 4)) {  // list slots of the roots, for the border descriptor
-      if (lF) s_li[F] = (uint16_t)iF;
-      if (lL) s_li[L] = (uint16_t)iL;
-      if (lR) s_li[R] = (uint16_t)iR;
-    }
     // throughput mode: a listed root's own word names its list slot (kListBit | slot)
-    // until k_ccl_merge overwrites it with the component's root (the merge finds a
-    // node's slot in two hops: node -> local root -> slot)
+    // until k_ccl_merge overwrites it with the component's root
     auto word = [&](uint32_t r, uint32_t w, uint32_t c, bool listed, uint32_t li) -> uint32_t {
       return (kKeep && listed) ? kListBit | li : gid(r) | fin(w, c);
     };
@@ -703,15 +712,13 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
       else size[idL + 1] = cR;
     }
   }
-  __syncthreads();
-  ph(9);
   if constexpr (TWD == 64 && !(AT_TC_EXP & 1)) {
     // throughput mode: the tile's border descriptor for k_ccl_merge (CclDesc) --
     // the threshold bytes of its outer rows / columns and the list slots of the
     // roots of its border blocks' nodes (a node with pixels in a border block
     // belongs to a listed root), so the merge reads whole descriptors instead of
-    // scattered threshold bytes and parent words
-    const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+    // scattered threshold bytes and parent words.  Issued before the last barrier,
+    // beside the other stores (after it, their latency lengthened every workgroup)
     uint32_t* dw = b.cdesc + tl * CclDesc::kWords;
     // whole-word stores: a wave holds two block rows, so the slots of blocks (x, x+1)
     // of a row are in lanes l, l+1 and those of block rows (2i, 2i+1) of a column in
@@ -752,6 +759,8 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) void k_thr_ccl(DevBufs b, Geom g,
           s_t[r][c] | (s_t[r + 1][c] << 8) | (s_t[r + 2][c] << 16) | ((uint32_t)s_t[r + 3][c] << 24);
     }
   }
+  __syncthreads();
+  ph(9);
   if (tid == 0) {
     b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
     kt_end(b, 1);
@@ -1257,11 +1266,21 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
   }
 }
 
+// SGPR budget (experiment builds: -DAT_BND_SGPRS=N): at .sgpr_count 106 a CU admits
+// 6 of these 4-wave workgroups (800 / (112 + 16)); capped at 80 it admits 8 (the
+// 19.5 KB of LDS allows 8 too): k_boundary 0.250 -> 0.236 ms per 128 frames
+// serialized, but 2 % less concurrent throughput -- eight workgroups take a CU's
+// whole LDS from the other batches' kernels (profiles/r04d/ab_sgpr_caps_stages.txt)
+#ifdef AT_BND_SGPRS
+#define AT_BND_ATTR __attribute__((amdgpu_num_sgpr(AT_BND_SGPRS)))
+#else
+#define AT_BND_ATTR
+#endif
 // KEPT (throughput mode): the size test comes with the root word (k_ccl_keep);
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
 template <bool KEPT>
-__global__ __launch_bounds__(256) void k_boundary(DevBufs b, Geom g) {
+__global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g) {
   __shared__ uint64_t s_pkey[kLdsPairSlots];
   __shared__ uint32_t s_pcnt[kLdsPairSlots];
   // points staged in LDS up to kBndStage (typical tiles hold ~0.7 points per
