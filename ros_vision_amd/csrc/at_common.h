@@ -232,9 +232,8 @@ struct DevBufs {
   uint32_t* nlroot;   // [B][CTX*CTY]
   uint32_t* lcnt;     // [B][CTX*CTY][kCclTileNodesMax] pixel count of each listed local root
   uint32_t* cdesc;    // [B][CTX*CTY][CclDesc::kWords] border descriptors (throughput mode)
-  uint32_t* ccl_ovf;  // [B] (control block) frames whose listed local roots exceeded k_ccl_merge's LDS:
-                      //     k_ccl_border / k_ccl_roots / k_ccl_keep resolve them (every frame when
-                      //     merge_cap == 0)
+  uint32_t* ccl_ovf;  // [B] (control block) frames whose listed local roots exceeded k_ccl_merge's LDS
+                      //     (k_ccl_merge resolves them in global memory: slow, rare)
   uint32_t* nlr_tot;  // [B] (control block) listed local roots of the frame (k_ccl_merge; statistics)
   uint32_t* size;     // [B][Wd*Hd]
   uint64_t* pts;      // [B][ntb][kBndPts] boundary points of each k_boundary tile, emission order

@@ -664,7 +664,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
                  wR = inimg && rR == R ? s_cnt[R] : 0u;
   const uint32_t cF = wF & ~kTouchBit, cL = wL & ~kTouchBit, cR = wR & ~kTouchBit;
   // the tile's local roots of components reaching its border (with pixels), listed for
-  // the cross-tile merge (k_ccl_merge; k_ccl_border / k_ccl_roots / k_ccl_keep)
+  // the cross-tile merge (k_ccl_merge in throughput mode, k_ccl_border + k_ccl_roots in latency mode)
   const bool lF = cF && (wF & kTouchBit), lL = cL && (wL & kTouchBit), lR = cR && (wR & kTouchBit);
   const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
                  iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
@@ -688,8 +688,8 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
     const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
     const uint32_t idL = idF + g.Wd;
-    // a root of a tile-interior component is final: in throughput mode (k_ccl_keep
-    // follows) its parent word gets the kept bit here and it is not listed
+    // a root of a tile-interior component is final: in throughput mode (k_ccl_merge
+    // sets the others' kept bits) its parent word gets the kept bit here and it is not listed
     auto fin = [&](uint32_t w, uint32_t c) -> uint32_t {
       return (kKeep && c && !(w & kTouchBit) && c >= 25) ? kKeptBit : 0u;
     };
@@ -826,22 +826,20 @@ __device__ void g_union2(uint32_t* par, uint32_t a, uint32_t b) {
   }
 }
 
+// Candidate cross-tile union t (0 .. BorderRoles::NT) of CCL tile (tx, ty) of frame
+// f: the reference's Merge test on the threshold plane, then a global union.
 template <int TWD>
-__global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, Geom g) {
+__device__ __forceinline__ void border_candidate(const DevBufs& b, const Geom& g, int f, int tx, int ty, int t) {
   constexpr int kBorderTop = BorderRoles<TWD>::Top, kBorderLeft = BorderRoles<TWD>::Left,
                 kBorderRight = BorderRoles<TWD>::Right;
   constexpr int kCclBW = CclTile<TWD>::BW, kCclBH = CclTile<TWD>::BH;
-  const int f = blockIdx.z;
-  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
-  if (!g.merge_cap) kt_begin(b, 2);
-  const int t = threadIdx.x;
   int bty = 0, btx = 0, role = 3, kind = 0;  // role 3: no candidate (padding threads)
   if (t < kBorderTop) { role = 0; bty = 0; btx = t / 5; kind = t % 5; }
   else if (t < kBorderTop + kBorderLeft) { role = 1; bty = (t - kBorderTop) / 3; btx = 0; kind = (t - kBorderTop) % 3; }
   else if (t < kBorderTop + kBorderLeft + kBorderRight) {
     role = 2; bty = t - (kBorderTop + kBorderLeft) + 1; btx = kCclBW - 1; kind = 0;
   }
-  const int BY = blockIdx.y * kCclBH + bty, BX = blockIdx.x * kCclBW + btx;
+  const int BY = ty * kCclBH + bty, BX = tx * kCclBW + btx;
   if (BY >= g.BH || BX >= g.BW) role = 3;
   const uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -879,9 +877,16 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
     link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
   }
   if (link) g_union2(par, u, v);
-  if (b.kt_stage == 2 && !g.merge_cap) {  // (uniform: the timed launch only)
+}
+
+// latency mode: one workgroup per CCL tile, one thread per candidate
+template <int TWD>
+__global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, Geom g) {
+  kt_begin(b, 2);
+  border_candidate<TWD>(b, g, blockIdx.z, blockIdx.x, blockIdx.y, threadIdx.x);
+  if (b.kt_stage == 2) {  // (uniform: the timed launch only)
     __syncthreads();
-    if (t == 0) kt_end(b, 2);
+    if (threadIdx.x == 0) kt_end(b, 2);
   }
 }
 
@@ -895,7 +900,6 @@ __global__ __launch_bounds__(BorderRoles<TWD>::NT) void k_ccl_border(DevBufs b, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   const int f = blockIdx.y;
-  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + fo;
@@ -913,27 +917,6 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
   }
 }
 
-// Once every count has reached its root: each local root's parent word becomes
-// root | kept << 31 (kept: the component has >= 25 pixels, the BlobDiff size
-// test, apriltag_gpu.cu:331-337), so k_boundary reads label and size test in the
-// same two hops and never touches the size plane.  (Roots of components inside
-// one CCL tile got theirs from k_thr_ccl already and are not listed.)
-__global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
-  const int f = blockIdx.y;
-  if (g.merge_cap && !b.ccl_ovf[f]) return;  // merged by k_ccl_merge (uniform)
-  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.x;
-  const size_t fo = (size_t)f * g.Wd * g.Hd;
-  uint32_t* par = b.par + fo;
-  const uint32_t* size = b.size + fo;
-  const uint32_t n = b.nlroot[tl];
-  const uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
-  for (uint32_t k = threadIdx.x; k < n; k += 64) {
-    const uint32_t l = lr[k];
-    const uint32_t r = par[l];
-    par[l] = r | (size[r] >= 25 ? kKeptBit : 0u);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // K4+K5 in one workgroup per frame (throughput mode): the cross-tile merge of
 // the CCL (the reference's Merge across tiles and FinalLabeling's roots,
@@ -945,13 +928,18 @@ __global__ __launch_bounds__(64) void k_ccl_keep(DevBufs b, Geom g) {
 // candidate links (the same tests on the threshold plane); a node's slot is two
 // hops away (node -> local root, whose word k_thr_ccl set to kListBit | list
 // slot).  Then every listed root's word becomes root | kept (>= 25 pixels) and
-// the root's count its component's size: what k_ccl_roots + k_ccl_keep leave.
-// A frame with more listed roots than the LDS holds is handed back to those
-// kernels (words restored, ccl_ovf set).
+// the root's count its component's size (k_boundary then reads label and size
+// test in the same two hops and never touches the size plane).
+// A frame with more listed roots than the LDS holds is merged by the same
+// workgroup in global memory (k_ccl_border's unions, k_ccl_roots' pass, the kept
+// bits; ccl_ovf set).
 // ---------------------------------------------------------------------------
 constexpr int kMergePer = (kMergeCapMax + 1023) / 1024;  // listed roots per thread
 constexpr int kMergeItems = 2;                          // border blocks per thread per pass
 
+__device__ __forceinline__ uint32_t lcnt_of(const DevBufs& b, int f, int ntl, int t, uint32_t k) {
+  return b.lcnt[((size_t)f * ntl + t) * kCclTileNodesMax + k];
+}
 // (keys change under other threads' atomics: every read is a relaxed atomic load,
 // which the compiler may not reuse across iterations)
 __device__ __forceinline__ uint64_t key_load(uint64_t* p) {
@@ -993,7 +981,6 @@ template <int TWD>
 __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
   constexpr int kBW = CT::BW, kBH = CT::BH;
-  constexpr int kNB = kBW + kBH + (kBH - 1);  // border blocks with candidate links: top row, left, right column
   extern __shared__ uint64_t s_key[];          // [merge_cap] parent key (gid << 32 | slot)
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_key + g.merge_cap);  // [merge_cap] pixel counts
   uint16_t* s_tile = reinterpret_cast<uint16_t*>(s_cnt + g.merge_cap);  // [merge_cap] tile of each slot
@@ -1011,7 +998,6 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
   const size_t fo = (size_t)f * g.Wd * g.Hd;
   uint32_t* par = b.par + fo;
   uint32_t* size = b.size + fo;
-  const uint8_t* thr = b.thr + fo;
   const uint32_t* lroot = b.lroot + (size_t)f * ntl * kCclTileNodesMax;
   // (0) list sizes -> slot bases, and the tile of every slot
   const uint32_t nt = tid < ntl ? b.nlroot[(size_t)f * ntl + tid] : 0u;
@@ -1031,8 +1017,11 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     }
   __syncthreads();
   if (!fits) {
-    // too many for the LDS: plain root words back, the multi-workgroup kernels merge it
-    for (int t = tid >> 6; t < ntl; t += 16) {
+    // more listed roots than the LDS holds (fine checkers, noise): the same merge in
+    // global memory by this workgroup -- k_ccl_border's unions (atomicMin links on the
+    // parent words), then k_ccl_roots' pass and the kept bits over the lists.  Slow
+    // (one workgroup for the frame) but rare; the frame's result is the same.
+    for (int t = tid >> 6; t < ntl; t += 16) {  // plain root words back first
       const uint32_t n = s_base[t + 1] - s_base[t];
       for (uint32_t k = lane_id(); k < n; k += 64) {
         const uint32_t l = lroot[(size_t)t * kCclTileNodesMax + k];
@@ -1040,7 +1029,40 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
       }
     }
     if (tid == 0) b.ccl_ovf[f] = 1u;
-    if (tid == 0) kt_end(b, 2);
+    __threadfence();
+    __syncthreads();
+    constexpr int kNR = BorderRoles<TWD>::NT;
+    for (int j = tid; j < ntl * kNR; j += 1024) {
+      const int t = j / kNR;
+      border_candidate<TWD>(b, g, f, t % g.CTX, t / g.CTX, j % kNR);
+    }
+    __threadfence();
+    __syncthreads();
+    for (int t = tid >> 6; t < ntl; t += 16) {  // roots: local root -> component root, counts to it
+      const uint32_t n = s_base[t + 1] - s_base[t];
+      for (uint32_t k = lane_id(); k < n; k += 64) {
+        const uint32_t l = lroot[(size_t)t * kCclTileNodesMax + k];
+        const uint32_t r = g_find(par, l);
+        if (r != l) {
+          par[l] = r;
+          atomicAdd(size + r, lcnt_of(b, f, ntl, t, k));
+        }
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    for (int t = tid >> 6; t < ntl; t += 16) {  // kept bit
+      const uint32_t n = s_base[t + 1] - s_base[t];
+      for (uint32_t k = lane_id(); k < n; k += 64) {
+        const uint32_t l = lroot[(size_t)t * kCclTileNodesMax + k];
+        const uint32_t r = g_load(par + l);
+        par[l] = r | (g_load(size + r) >= 25 ? kKeptBit : 0u);
+      }
+    }
+    if (b.kt_stage == 2) {
+      __syncthreads();
+      if (tid == 0) kt_end(b, 2);
+    }
     return;
   }
   stamp(1);
@@ -1276,7 +1298,7 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 #else
 #define AT_BND_ATTR
 #endif
-// KEPT (throughput mode): the size test comes with the root word (k_ccl_keep);
+// KEPT (throughput mode): the size test comes with the root word (k_ccl_merge);
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
 template <bool KEPT>
@@ -1312,7 +1334,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   constexpr int kTR = 4 * kBndRows + 1, kTC = 66, kTN = kTR * kTC;
   constexpr int kPer = (kTN + 255) / 256;
   // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
-  // column) -> local root -> component root | kept bit (k_ccl_roots, k_ccl_keep;
+  // column) -> local root -> component root | kept bit (k_ccl_merge / k_ccl_roots;
   // a local root's own word already holds root | kept, so the second hop masks)
   // (the threshold byte and both candidate nodes' parents are loaded together,
   // the byte then picks fg or bg: one round trip fewer than thr -> node -> parent)
@@ -4720,19 +4742,13 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     tk(2, st, 0);
     if (!on(2)) {}
     else if (g.ctw == 32) hipLaunchKernelGGL(k_ccl_border<32>, grd, dim3(BorderRoles<32>::NT), 0, st, b, g);
-    else if (g.merge_cap) hipLaunchKernelGGL(k_ccl_merge<64>, dim3(B), dim3(1024), merge_lds_bytes(g), st, b, g, prm);
-    else hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
+    else hipLaunchKernelGGL(k_ccl_merge<64>, dim3(B), dim3(1024), merge_lds_bytes(g), st, b, g, prm);
     tk(2, st, 1);
-    // frames k_ccl_merge could not hold: the multi-workgroup merge (the others exit at once)
-    if (on(2) && g.ctw != 32 && g.merge_cap)
-      hipLaunchKernelGGL(k_ccl_border<64>, grd, dim3(BorderRoles<64>::NT), 0, st, b, g);
     mark();
   }
   tk(3, st, 0);
-  if (on(3)) {
+  if (on(3) && g.ctw == 32)  // (throughput mode: k_ccl_merge did it)
     hipLaunchKernelGGL(k_ccl_roots, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
-    if (g.ctw != 32) hipLaunchKernelGGL(k_ccl_keep, dim3(g.CTX * g.CTY, B), dim3(64), 0, st, b, g);
-  }
   tk(3, st, 1);
   mark();
   {

@@ -89,7 +89,7 @@ def test_batch_matches_single(gpu, oracle_mod):
 
 def test_throughput_mode_matches_oracle(gpu, oracle_mod):
     """max_batch >= 8 selects the throughput-mode kernels (64-wide CCL tiles,
-    k_ccl_keep + k_boundary<true>, k_extents for every candidate, k_blob_small
+    k_ccl_merge + k_boundary<true>, k_extents for every candidate, k_blob_small
     without fused extents, 256-thread large-blob teams): per-frame stages and
     detections identical to the oracle, as in latency mode."""
     from ros_vision_amd import synth
@@ -125,7 +125,7 @@ def test_partial_tile_geometries(gpu, oracle_mod, W, H, batch):
     bottom borders.  The reference's only geometry preconditions are W, H multiples of
     8 (threshold.cu:156-157) and even decimated sizes (labeling_allegretti_2019_BKE.cu:
     469-475).  Latency mode (batch 1: 32-wide CCL tiles, k_pre fused) and throughput
-    mode (batch 8: 64-wide tiles, k_extents, k_ccl_keep): every stage bit-exact."""
+    mode (batch 8: 64-wide tiles, k_ccl_merge, k_extents): every stage bit-exact."""
     from ros_vision_amd import synth
     codes = dict(oracle_mod.family_entries())
     frames = [synth.render_edge_board(W, H, seed=W + H + 7 * k, codes=codes) for k in range(min(batch, 3))]
@@ -461,7 +461,8 @@ def test_dense_frames_keep_every_candidate(gpu, oracle_mod, batch):
 def test_ccl_merge_and_fallback_in_one_batch(gpu, oracle_mod):
     """Throughput mode merges each frame's listed local roots in one workgroup's LDS
     (k_ccl_merge); a frame with more (white noise: thousands of tile-border specks)
-    goes to the multi-workgroup kernels (k_ccl_border / k_ccl_roots / k_ccl_keep).
+    is merged by the same workgroup in global memory (k_ccl_border's unions, k_ccl_roots'
+    pass and the kept bits).
     Both kinds of frame in one batch: every stage bit-exact against the oracle
     (labels = the component's minimum node id, labeling_allegretti_2019_BKE.cu:340-462)."""
     from ros_vision_amd import synth

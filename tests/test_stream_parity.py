@@ -78,7 +78,7 @@ def test_bench_headline_configuration(c2):
 
 def test_c4_1080p_throughput_mode(oracle_mod):
     """1920x1080, 24 tags, max_batch 8 (throughput-mode kernels: 64-wide CCL tiles,
-    k_ccl_keep + k_boundary<true>, k_extents for every candidate, 256-thread
+    k_ccl_merge + k_boundary<true>, k_extents for every candidate, 256-thread
     large-blob teams), frames resident in HBM."""
     import torch
 
