@@ -505,19 +505,20 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   for (int k = 0; k < kDecPer; k++) {
     const int i = tid + NT * k;
     const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
-    dv[k] = (i < kHR * kHC && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? dec[(size_t)y * g.Wd + x] : 0;
+    // unconditional load from the clamped address, select afterwards: no
+    // branch per load, so all kDecPer loads issue back to back
+    const int yc = min(max(y, 0), g.Hd - 1), xc = min(max(x, 0), g.Wd - 1);
+    const uint8_t v = dec[(size_t)yc * g.Wd + xc];
+    dv[k] = (i < kHR * kHC && y == yc && x == xc) ? v : 0;
   }
   for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
     const int r = i / (kTW + 4), c = i % (kTW + 4);
     const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
-    uint8_t mn = 255, mx = 0;  // out of range: neutral for min/max
-    if (tr >= 0 && tr < g.TH && tc >= 0 && tc < g.TW) {
-      const uint16_t v = *reinterpret_cast<const uint16_t*>(mm + 2 * ((size_t)tr * g.TW + tc));
-      mn = v & 0xff;
-      mx = v >> 8;
-    }
-    s_umn[r][c] = mn;
-    s_umx[r][c] = mx;
+    const int trc = min(max(tr, 0), g.TH - 1), tcc = min(max(tc, 0), g.TW - 1);
+    const uint16_t v = *reinterpret_cast<const uint16_t*>(mm + 2 * ((size_t)trc * g.TW + tcc));
+    const bool in = tr == trc && tc == tcc;  // out of range: neutral for min/max
+    s_umn[r][c] = in ? (uint8_t)(v & 0xff) : (uint8_t)255;
+    s_umx[r][c] = in ? (uint8_t)(v >> 8) : (uint8_t)0;
   }
   __syncthreads();
   ph(1);
