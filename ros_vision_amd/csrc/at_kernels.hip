@@ -109,6 +109,14 @@ struct AddOp {
   template <typename T> __device__ static T identity() { return T(0); }
 };
 
+// Length of the run of equal keys starting at this lane (only meaningful for
+// run heads); same_mask bit l means "lane l continues the run of lane l-1".
+__device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
+  if (lane == 63) return 1;
+  const uint64_t rest = ~(same_mask >> (lane + 1));
+  return 1 + (uint32_t)__builtin_ctzll(rest);
+}
+
 // ---- block reductions (256 threads = 4 waves) ------------------------------
 template <typename T, typename Op>
 __device__ T wave_reduce(T v, Op op) {
@@ -643,16 +651,28 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   s_par[R] = rR;
   const uint32_t nfg = (a == 255) + (bb == 255) + (c == 255) + (d == 255);
   const uint32_t nbl = (a == 0) + (c == 0), nbr = (bb == 0) + (d == 0);
-  if (nfg) atomicAdd(&s_cnt[rF], nfg);
-  if (nbl) atomicAdd(&s_cnt[rL], nbl);
-  if (nbr) atomicAdd(&s_cnt[rR], nbr);
   // components reaching a border block may be merged across tiles (k_ccl_border);
   // every other component is complete here: root and pixel count are final
-  if (bty == 0 || bty == CT::BH - 1 || btx == 0 || btx == kCclBW - 1) {
-    if (nfg) atomicOr(&s_cnt[rF], kTouchBit);
-    if (nbl) atomicOr(&s_cnt[rL], kTouchBit);
-    if (nbr) atomicOr(&s_cnt[rR], kTouchBit);
-  }
+  const bool edge = bty == 0 || bty == CT::BH - 1 || btx == 0 || btx == kCclBW - 1;
+  // runs of equal roots in consecutive lanes add their pixels with one atomic by the
+  // run's head (same-address LDS atomics from a run's lanes serialize)
+  auto count = [&](uint32_t r, uint32_t n) {
+    const uint32_t key = n ? r : 0xffffffffu;
+    const bool same = n && wave_shr1(key, 0xfffffffeu) == key;
+    const uint64_t sm = __ballot(same), em = __ballot(edge && n);
+    const uint32_t incl = wave_incl_scan(n, AddOp(), 0u);
+    const bool head = n && !same;
+    const uint32_t len = head ? run_len(sm, lane) : 1u;
+    const uint32_t last = (uint32_t)__shfl((int)incl, (int)(lane + len - 1));
+    if (head) {
+      atomicAdd(&s_cnt[r], last - incl + n);
+      const uint64_t run = len == 64 ? ~0ull : ((1ull << len) - 1);
+      if ((em >> lane) & run) atomicOr(&s_cnt[r], kTouchBit);
+    }
+  };
+  count(rF, nfg);
+  count(rL, nbl);
+  count(rR, nbr);
   __syncthreads();
   ph(8);
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
@@ -1229,13 +1249,6 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// Length of the run of equal keys starting at this lane (only meaningful for
-// run heads); same_mask bit l means "lane l continues the run of lane l-1".
-__device__ __forceinline__ uint32_t run_len(uint64_t same_mask, uint32_t lane) {
-  if (lane == 63) return 1;
-  const uint64_t rest = ~(same_mask >> (lane + 1));
-  return 1 + (uint32_t)__builtin_ctzll(rest);
-}
 
 __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uint64_t key, uint32_t len) {
   uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
