@@ -3741,6 +3741,80 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
   }
 }
 
+// One team of NT threads over the large work list (dynamic dequeue, longest first:
+// large blobs vary 8x in cost, and there are few of them, so one atomic per item
+// is cheap); `slot` indexes the team's global sort scratch.
+template <int NT, int CAP, bool FUSE>
+__device__ __forceinline__ void large_blob_loop(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S,
+                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t nlo, uint32_t slot) {
+  const int tid = threadIdx.x;
+  uint32_t* pacc = S.pacc;
+  if (tid < 22) pacc[tid] = 0;
+  if (tid == 0) S.slow_dt = 0;
+  uint64_t* gpk = b.s_pk + (size_t)slot * (kSortCap / 2);
+  __syncthreads();
+  const int ncls = nlo ? 1 : g.nlarge;  // (blobs over 4096 points are all in class 0)
+  uint32_t nwork = 0;
+  for (int c = 0; c < ncls; c++) nwork += s_cnt[c];
+  uint32_t* head = nlo ? b.workhead_small : b.workhead;
+  while (true) {
+    if (tid == 0) S.item = atomicAdd(head, 1u);
+    __syncthreads();
+    const uint32_t item = S.item;
+    __syncthreads();
+    if (item >= nwork) break;
+    uint32_t w = 0;
+    work_item(b, s_cnt, 0, ncls, item, &w);
+    const PairInfo pi = FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w);
+    if (pi.n > (uint32_t)CAP || pi.n <= nlo) continue;  // the other launch's item (uniform)
+    blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, pi, pacc);
+  }
+  __syncthreads();
+  probe_flush(b, prm, pacc, 80, tid == 0);
+  probe_flush_slow(b, prm, S, tid == 0);
+  if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
+  if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+}
+
+// One wave over the small work list: wave `wv` of `nwaves` takes items wv, wv +
+// nwaves, ... (static round-robin over the size-ordered list: no dequeue atomic --
+// a device-scope atomic on one hot address is serviced at the memory side; one per
+// small blob serialized every wave of the chip behind that address).  Software
+// pipeline: the work entry two items ahead and the pair-table entries one item
+// ahead are in flight while a blob is processed.
+template <bool FUSE>
+__device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<64, kSmallBlob>& S,
+                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t wv, uint32_t nwaves) {
+  const uint32_t lane = lane_id();
+  uint32_t* pacc = S.pacc;
+  if (lane < 22) pacc[lane] = 0;
+  if (lane == 0) S.slow_dt = 0;
+  uint32_t nwork = 0;
+  for (int c = g.nlarge; c < kNumCls; c++) nwork += s_cnt[c];
+  uint32_t item = wv;
+  uint32_t w = 0, w1 = 0;
+  PairInfo pi = {0, 0, 0};
+  if (item < nwork) {
+    work_item(b, s_cnt, g.nlarge, kNumCls, item, &w);
+    pi = load_pair_info(b, w);
+  }
+  if (item + nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + nwaves, &w1);
+  for (; item < nwork; item += nwaves) {
+    const bool has1 = item + nwaves < nwork;
+    const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
+    uint32_t w2 = 0;
+    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + 2 * nwaves, &w2);
+    [[clang::always_inline]] blob_item<64, kSmallBlob, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
+    w = w1;
+    pi = pi1;
+    w1 = w2;
+  }
+  probe_flush(b, prm, pacc, 64, lane == 0);
+  probe_flush_slow(b, prm, S, lane == 0);
+  if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
+  if (lane == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+}
+
 // K9a (large blobs, > kSmallBlob points): one blob per NT-thread workgroup
 // iteration, persistent over the large work list.  Geometries whose blobs can
 // exceed 4096 points (max_cluster = 2 (W + H) > 4096, e.g. 1080p) run two
@@ -3763,37 +3837,10 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
     kt_slot = atomicAdd(b.kgrid, 1u);
     if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
   }
-  uint32_t* pacc = S.pacc;
-  if (tid < 22) pacc[tid] = 0;
-  if (tid == 0) S.slow_dt = 0;
-  uint64_t* gpk = b.s_pk + (size_t)blockIdx.x * (kSortCap / 2);
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, tid, NT);
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
-  __syncthreads();
-  const int ncls = nlo ? 1 : g.nlarge;  // (blobs over 4096 points are all in class 0)
-  uint32_t nwork = 0;
-  for (int c = 0; c < ncls; c++) nwork += s_cnt[c];
-  uint32_t* head = nlo ? b.workhead_small : b.workhead;
-  // dynamic dequeue over the size-ordered list (longest first): large blobs
-  // vary 8x in cost, and there are few of them, so one atomic per item is cheap
-  while (true) {
-    if (tid == 0) S.item = atomicAdd(head, 1u);
-    __syncthreads();
-    const uint32_t item = S.item;
-    __syncthreads();
-    if (item >= nwork) break;
-    uint32_t w = 0;
-    work_item(b, s_cnt, 0, ncls, item, &w);
-    const PairInfo pi = FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w);
-    if (pi.n > (uint32_t)CAP || pi.n <= nlo) continue;  // the other launch's item (uniform)
-    blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, pi, pacc);
-  }
-  __syncthreads();
-  probe_flush(b, prm, pacc, 80, tid == 0);
-  probe_flush_slow(b, prm, S, tid == 0);
-  if (tid == 0 && pacc[20]) atomicAdd(b.blob_pts + 1, pacc[20]);
-  if (tid == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+  large_blob_loop<NT, CAP, FUSE>(b, g, prm, S, s_combo, s_cnt, nlo, blockIdx.x);
   if (tid == 0 && !nlo) kt_end(b, 9);
   if (tid == 0 && nlo && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
 }
@@ -3808,49 +3855,44 @@ template <bool FUSE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : AT_BS_WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm) {
   __shared__ BlobShared<64, kSmallBlob> Ss[4];
   const int wave = threadIdx.x >> 6;
-  const uint32_t lane = lane_id();
-  BlobShared<64, kSmallBlob>& S = Ss[wave];
   kt_begin(b, 8);
-  uint32_t* pacc = S.pacc;
-  if (lane < 22) pacc[lane] = 0;
-  if (lane == 0) S.slow_dt = 0;
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, threadIdx.x, 256);
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
   __syncthreads();
-  uint32_t nwork = 0;
-  for (int c = g.nlarge; c < kNumCls; c++) nwork += s_cnt[c];
-  // static round-robin over the size-ordered list: no dequeue atomic (a
-  // device-scope atomic on one hot address is serviced at the memory side; one
-  // per small blob serialized every wave of the chip behind that address)
-  // software pipeline over the wave's items: the work entry two items ahead and
-  // the pair-table entries one item ahead are in flight while a blob is processed
-  const uint32_t nwaves = gridDim.x * 4;
-  uint32_t item = blockIdx.x * 4 + wave;
-  uint32_t w = 0, w1 = 0;
-  PairInfo pi = {0, 0, 0};
-  if (item < nwork) {
-    work_item(b, s_cnt, g.nlarge, kNumCls, item, &w);
-    pi = load_pair_info(b, w);
-  }
-  if (item + nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + nwaves, &w1);
-  for (; item < nwork; item += nwaves) {
-    const bool has1 = item + nwaves < nwork;
-    const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
-    uint32_t w2 = 0;
-    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + 2 * nwaves, &w2);
-    blob_item<64, kSmallBlob, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
-    w = w1;
-    pi = pi1;
-    w1 = w2;
-  }
-  probe_flush(b, prm, pacc, 64, lane == 0);
-  probe_flush_slow(b, prm, S, lane == 0);
-  if (lane == 0 && pacc[20]) atomicAdd(b.blob_pts + 0, pacc[20]);
-  if (lane == 0 && pacc[21]) atomicAdd(b.nquads, pacc[21]);  // batch total in nquads[0]
+  small_blob_loop<FUSE>(b, g, prm, Ss[wave], s_combo, s_cnt, blockIdx.x * 4 + wave, gridDim.x * 4);
   if (b.kt_stage == 8) {  // (uniform: the timed launch only)
     __syncthreads();
     if (threadIdx.x == 0) kt_end(b, 8);
+  }
+}
+
+// Latency mode (blobs of up to 4096 points): the large-blob teams and the small-blob
+// waves in ONE launch, so the B = 1 chain has no fork / join between two kernels on
+// two streams (their event edges cost ~15 us).  Even workgroups are 512-thread
+// large-blob teams, odd ones eight small-blob waves each (in the large team's LDS);
+// extents, SelectBlobs and keys inside both (FUSE).
+__global__ __launch_bounds__(512) void k_blob_lat(DevBufs b, Geom g, Params prm) {
+  using SL = BlobShared<512, 4096>;
+  using SS = BlobShared<64, kSmallBlob>;
+  static_assert(8 * sizeof(SS) <= sizeof(SL), "eight small-blob waves fit in a large team's LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[sizeof(SL)];
+  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  const int tid = threadIdx.x;
+  kt_begin(b, 9);
+  load_combos(s_combo, tid, 512);
+  if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
+  const uint32_t team = blockIdx.x >> 1, nteam = gridDim.x >> 1;
+  if ((blockIdx.x & 1) == 0) {
+    large_blob_loop<512, 4096, true>(b, g, prm, *reinterpret_cast<SL*>(s_raw), s_combo, s_cnt, 0u, team);
+  } else {
+    __syncthreads();
+    const int wave = tid >> 6;
+    small_blob_loop<true>(b, g, prm, reinterpret_cast<SS*>(s_raw)[wave], s_combo, s_cnt, team * 8 + wave, nteam * 8);
+  }
+  if (b.kt_stage == 9) {  // (uniform: the timed launch only)
+    __syncthreads();
+    if (tid == 0) kt_end(b, 9);
   }
 }
 
@@ -4789,6 +4831,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   // k_extents: the fused small-blob kernel needs 2 waves/SIMD, or spills at 4, and
   // measured 1-5 % slower in concurrent throughput, profiles/r03h, r03i.)
   const bool fuse_small = g.ctw == 32;
+  // latency mode with blobs of up to 4096 points: k_blob_lat holds both kinds (stage
+  // profiling and the kernel timer keep the two kernels, to time them apart)
+  const bool lat_fused = g.ctw == 32 && g.max_cluster <= 4096 && !ev && !kt;
   if (on(7) && !(g.ctw == 32 && g.max_cluster <= 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
   tk(7, st, 1);
   mark();
@@ -4797,7 +4842,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     // LDS sized for the largest blob the geometry admits (max_cluster = 2 (W + H))
     const bool cap4k = g.max_cluster <= 4096;
     if (!on(9)) return;
-    if (g.ctw == 32 && cap4k) {  // latency mode: extents, SelectBlobs and keys in the blob team (no k_extents)
+    if (lat_fused) {  // latency mode: both blob kinds in one launch (no k_extents, no fork / join)
+      hipLaunchKernelGGL(k_blob_lat, dim3(nblobwg), dim3(512), 0, s, b, g, prm);
+    } else if (g.ctw == 32 && cap4k) {  // latency mode, timed apart: extents, SelectBlobs and keys in the team
       hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
     } else if (B < kWideBlobMaxBatch || prm.wide_blob) {  // (latency: one launch, longest blob first)
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
@@ -4810,12 +4857,12 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   };
   auto blob_small = [&](hipStream_t s) {
     tk(8, s, 0);
-    if (!on(8)) {}
+    if (!on(8) || lat_fused) {}
     else if (fuse_small) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
     else hipLaunchKernelGGL(k_blob_small<false>, dim3(prm.sblob_wg ? prm.sblob_wg : nblobwg * 2), dim3(256), 0, s, b, g, prm);
     tk(8, s, 1);
   };
-  if (ev || !st2) {
+  if (ev || !st2 || lat_fused) {
     blob_small(st);
     mark();
     blob_large(st);
