@@ -1989,27 +1989,42 @@ __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
     }
   }
   __syncthreads();
-  auto place = [&](uint64_t key) {
+  // called by every lane of the wave (valid: the lane holds a point); runs of equal
+  // entries in consecutive lanes reserve their slots with one LDS atomic by the head
+  const uint32_t lane = lane_id();
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  auto place = [&](uint64_t key, bool valid) {
     const uint64_t r01 = key >> 24;
-    uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
     uint32_t e = 0xffffffffu;
-    for (int probe = 0; probe < 2 * kGrpEnt; probe++) {
-      const uint64_t k = s_hk[h];
-      if (k == r01) { e = s_he[h]; break; }
-      if (k == 0) break;
-      h = (h + 1) & (2 * kGrpEnt - 1);
+    if (valid) {
+      uint32_t h = (uint32_t)(mix_hash(r01) & (2 * kGrpEnt - 1));
+      for (int probe = 0; probe < 2 * kGrpEnt; probe++) {
+        const uint64_t k = s_hk[h];
+        if (k == r01) { e = s_he[h]; break; }
+        if (k == 0) break;
+        h = (h + 1) & (2 * kGrpEnt - 1);
+      }
     }
-    if (e != 0xffffffffu) {
-      if (s_base[e] == kGrpDrop) return;
-      grp[s_base[e] + atomicAdd(&s_cur[e], 1u)] = (uint32_t)key & 0xffffffu;
-    } else {
-      place_global(r01, (uint32_t)key & 0xffffffu);
-    }
+    const uint32_t base = e != 0xffffffffu ? s_base[e] : kGrpDrop;
+    const bool lds = base != kGrpDrop;
+    const uint32_t ek = lds ? e : 0x80000000u + lane;  // (never equal to a neighbour's)
+    const bool same = lds && wave_shr1(ek, 0xffffffffu) == ek;
+    const uint64_t same_mask = __ballot(same);
+    const bool head = lds && !same;
+    uint32_t start = 0;
+    if (head) start = atomicAdd(&s_cur[e], run_len(same_mask, lane));
+    const uint64_t heads = __ballot(head);
+    const int hl = (heads & le) ? 63 - __builtin_clzll(heads & le) : (int)lane;
+    const uint32_t s0 = (uint32_t)__shfl((int)start, hl);
+    if (lds) grp[base + s0 + (lane - (uint32_t)hl)] = (uint32_t)key & 0xffffffu;
+    else if (valid && e == 0xffffffffu) place_global(r01, (uint32_t)key & 0xffffffu);
   };
 #pragma unroll
-  for (int k = 0; k < kGrpPre; k++)
-    if ((uint32_t)(tid + 256 * k) < n) place(pv[k]);
-  for (uint32_t i = tid + 256 * kGrpPre; i < n; i += 256) place(pts[i]);
+  for (int k = 0; k < kGrpPre; k++) place(pv[k], (uint32_t)(tid + 256 * k) < n);
+  for (uint32_t i0 = 256 * kGrpPre; i0 < n; i0 += 256) {
+    const uint32_t i = i0 + tid;
+    place(i < n ? pts[i] : 0ull, i < n);
+  }
 }
 
 // ---------------------------------------------------------------------------
