@@ -1,4 +1,6 @@
+#!/bin/bash
 # k_pre + k_thr_ccl only (AT_DIAG_PIPE_STOP=2, experiment builds): concurrent cost of k_thr_ccl variants
+#   LIBS="libat_a.so libat_b.so" (under ros_vision_amd/ab/) [PS=2] bash tools/ps2_ab.sh
 O=gpurun_out/ps2; mkdir -p $O
 for r in 1 2; do for lib in $LIBS; do
   echo -n "r=$r $lib " >> $O/r.txt
