@@ -3598,7 +3598,10 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
   int64_t spg = 0;
   // U points per lane per round, every load of a round issued before any is
   // used; the first round's keys stay in registers for the key pass below
-  constexpr int U = 8;
+#ifndef AT_EXT_U
+#define AT_EXT_U 4
+#endif
+  constexpr int U = AT_EXT_U;
   uint32_t kr[U];
   for (uint32_t base = 0; base < n; base += NT * U) {
     uint32_t kk[U];
@@ -3704,8 +3707,14 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 
 // Large candidates (size classes 0-2) one per workgroup, then small ones one
 // per wave.
+// 6 waves per SIMD (80 VGPRs with 4 points per lane in flight) and a grid that fills
+// them: k_extents 0.152 -> 0.131 ms per 128 frames against 4 waves / 8 points per lane
+// (127 VGPRs), concurrent throughput unchanged or better (profiles/r04n, r04o)
 #ifndef AT_EXT_WAVES
-#define AT_EXT_WAVES 4
+#define AT_EXT_WAVES 6
+#endif
+#ifndef AT_EXT_GRID
+#define AT_EXT_GRID 1536  // workgroups (persistent over the candidates): AT_EXT_WAVES x 256 CUs / 4
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVES))) void k_extents(DevBufs b, Geom g) {
   __shared__ int64_t s_red[4][8];
@@ -4849,7 +4858,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   // latency mode with blobs of up to 4096 points: k_blob_lat holds both kinds (stage
   // profiling and the kernel timer keep the two kernels, to time them apart)
   const bool lat_fused = g.ctw == 32 && g.max_cluster <= 4096 && !ev && !kt;
-  if (on(7) && !(g.ctw == 32 && g.max_cluster <= 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(1024, 96 * B))), dim3(256), 0, st, b, g);
+  if (on(7) && !(g.ctw == 32 && g.max_cluster <= 4096)) hipLaunchKernelGGL(k_extents, dim3(std::max(16, std::min(AT_EXT_GRID, 96 * B))), dim3(256), 0, st, b, g);
   tk(7, st, 1);
   mark();
   auto blob_large = [&](hipStream_t s) {
