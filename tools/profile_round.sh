@@ -9,7 +9,7 @@
 # Output: gpurun_out/$TAG/...   usage: bash tools/profile_round.sh TAG [BATCH]
 set -euo pipefail
 TAG=${1:-prof}
-BATCH=${2:-128}
+BATCH=${2:-192}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"

@@ -9,6 +9,6 @@ for cfg in "${LIST[@]}"; do
   echo -n "inst=$inst batch=$batch hwq=$hwq " >> $OUT/r.txt
   timeout -k 10 150 python3 bench.py --instances $inst --batch $batch --hw-queues $hwq --pool 128 --steps ${STEPS:-40} --warmup 5 \
     --no-cpu-baseline --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 --no-stage-profile --no-kernel-timer 2>>$OUT/err.txt \
-    | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['value'], j['ms_per_step'], j.get('host_us_per_step'))" >> $OUT/r.txt || exit 1
+    | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['value'], j['ms_per_step'], j.get('detections_per_frame'), j.get('host_us_per_step'))" >> $OUT/r.txt || exit 1
 done
 cat $OUT/r.txt
