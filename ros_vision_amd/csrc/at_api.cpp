@@ -326,6 +326,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   // frames list ~40), at most what 160 KiB hold; latency mode keeps the
   // multi-workgroup border / roots kernels (one frame: their parallelism is the chain)
   g.merge_cap = g.ctw == 64 ? std::min(kMergeCapMax, 80 * g.CTX * g.CTY) : 0;
+  g.merge_lds = std::min(g.merge_cap * 14, kMergeLdsMax);
   if (g.CTX * g.CTY > kMaxCclTiles) {
     at_destroy(d);
     return AT_E_INVALID;

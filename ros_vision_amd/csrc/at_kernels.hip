@@ -1002,9 +1002,13 @@ template <int TWD>
 __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
   constexpr int kBW = CT::BW, kBH = CT::BH;
-  extern __shared__ uint64_t s_key[];          // [merge_cap] parent key (gid << 32 | slot)
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_key + g.merge_cap);  // [merge_cap] pixel counts
-  uint16_t* s_tile = reinterpret_cast<uint16_t*>(s_cnt + g.merge_cap);  // [merge_cap] tile of each slot
+  // LDS laid out by the frame's number of listed roots (total): parent keys (gid << 32 |
+  // slot), the tile of each slot and, when 14 B per root fit, the pixel counts; a frame
+  // whose counts do not fit (1080p noise: ~11 k roots) sums them in the size plane at L2
+  // instead (10 B per root: up to 15,360 roots)
+  extern __shared__ uint64_t s_key[];          // [total] parent key
+  uint16_t* s_tile = nullptr;                  // [total] tile of each slot
+  uint32_t* s_cnt = nullptr;                   // [total] pixel counts (cnt_lds)
   __shared__ uint32_t s_base[kMaxCclTiles + 1];
   __shared__ uint32_t s_wsum[16];
   const int f = blockIdx.x;
@@ -1030,6 +1034,9 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     b.nlr_tot[f] = total;
   }
   const bool fits = total <= (uint32_t)g.merge_cap;
+  const bool cnt_lds = (size_t)total * 14 + 4 <= (size_t)g.merge_lds;
+  s_tile = reinterpret_cast<uint16_t*>(s_key + total);
+  s_cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_key) + (((size_t)total * 10 + 3) & ~(size_t)3));
   __syncthreads();  // s_base complete
   if (fits)
     for (int t = tid >> 6; t < ntl; t += 16) {  // a wave per tile
@@ -1098,7 +1105,7 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
       const int t = s_tile[i];
       const size_t e = (size_t)t * kCclTileNodesMax + (i - s_base[t]);
       mg[j] = lroot[e];
-      s_cnt[i] = lcnt[e];
+      if (cnt_lds) s_cnt[i] = lcnt[e];
       s_key[i] = ((uint64_t)mg[j] << 32) | i;
     }
   }
@@ -1187,15 +1194,25 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
   }
   __syncthreads();
   stamp(3);
-  // (3) component sizes at the roots
+  // (3) component sizes at the roots: in LDS, or (counts not in LDS) every listed non-root
+  // adds its local count to the size word of its component's root, which holds the
+  // root's own local count (k_thr_ccl)
 #pragma unroll
   for (int j = 0; j < kMergePer; j++) {
     const uint32_t i = tid + 1024u * j;
     if (i < total) {
       const uint32_t r = merge_find(s_key, i);
-      if (r != i) atomicAdd(&s_cnt[r], s_cnt[i]);
+      if (r != i) {
+        if (cnt_lds) {
+          atomicAdd(&s_cnt[r], s_cnt[i]);
+        } else {
+          const int t = s_tile[i];
+          atomicAdd(size + (uint32_t)(key_load(s_key + r) >> 32), lcnt[(size_t)t * kCclTileNodesMax + (i - s_base[t])]);
+        }
+      }
     }
   }
+  if (!cnt_lds) __threadfence();  // (the adds done at L2 before any lane reads a size back)
   __syncthreads();
   stamp(4);
   // (4) every listed root's word: root | kept; the root's count: its component's size
@@ -1204,10 +1221,10 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     const uint32_t i = tid + 1024u * j;
     if (i < total) {
       const uint32_t r = merge_find(s_key, i);  // (one hop after (3)'s halving, mostly)
-      const uint32_t n = s_cnt[r];
       const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
+      const uint32_t n = cnt_lds ? s_cnt[r] : g_load(size + root);
       par[mg[j]] = root | (n >= 25 ? kKeptBit : 0u);
-      if (r == i) size[mg[j]] = n;
+      if (cnt_lds && r == i) size[mg[j]] = n;
     }
   }
   stamp(5);
@@ -4769,7 +4786,7 @@ hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bg
   return hipGetLastError();
 }
 
-static size_t merge_lds_bytes(const Geom& g) { return (size_t)g.merge_cap * 14; }
+static size_t merge_lds_bytes(const Geom& g) { return (size_t)g.merge_lds; }
 
 // one-time kernel attributes: k_ccl_merge's dynamic LDS beyond the default limit
 hipError_t prepare_kernels(const Geom& g) {
