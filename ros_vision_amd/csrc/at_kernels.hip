@@ -4058,6 +4058,11 @@ __device__ void decode_finish(const DevBufs& b, int lane, uint32_t nq) {
     b.hctrl[w] = __hip_atomic_load(b.ctrl + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#ifndef AT_BIG_BLOB_WG
+#define AT_BIG_BLOB_WG 256  // workgroups of the CAP-8192 large-blob launch (blobs over 4096 points):
+// one per CU -- 64 left the 1080p stage at 4.03 ms per 192 frames serialized, 1.69 ms at 256
+// (concurrent 1080p throughput +1.5 %, profiles/r04y)
+#endif
 #ifndef AT_FORK_SMALL
 #define AT_FORK_SMALL 1  // latency mode: fork the small-blob kernel (0: the large-blob one)
 #endif
@@ -4895,7 +4900,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
     } else {
       hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u);
-      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, 64)), dim3(256), 0, s, b, g, prm, 4096u);
+      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(256), 0, s, b, g, prm, 4096u);
     }
     tk(9, s, 1);
   };
