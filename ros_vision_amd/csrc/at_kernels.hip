@@ -1408,42 +1408,52 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   for (int r = 0; r < kBndRows; r++) {
     const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
     const int y = ty0 + ly;
-    uint64_t pk[4] = {0, 0, 0, 0};
+    // the pixel's points: a direction mask and the neighbour labels (the keys are built
+    // only where stored); a point's b2w is v0 == 0 (its neighbour is 255 - v0)
+    uint32_t hm = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0, rep0 = 0;
+    bool b2w = false;
     if (x <= g.Wd - 2 && y <= g.Hd - 2) {
       const int e0 = ly * kTC + threadIdx.x + 1;
       const uint8_t v0 = s_tthr[e0];
       if (v0 != 127) {
-        const uint32_t rep0 = s_tlab[e0];
+        rep0 = s_tlab[e0];
+        b2w = v0 == 0;
         const int er = e0 + 1, ed = e0 + kTC, edr = ed + 1, edl = ed - 1, el = e0 - 1;
         const uint8_t vr = s_tthr[er], vd = s_tthr[ed], vdr = s_tthr[edr], vdl = s_tthr[edl], vl = s_tthr[el];
-        if (v0 + vr == 255) pk[0] = make_qbp(rep0, s_tlab[er], x, y, 0, vr > v0);
-        if (v0 + vdr == 255) pk[1] = make_qbp(rep0, s_tlab[edr], x, y, 1, vdr > v0);
-        if (v0 + vd == 255) pk[2] = make_qbp(rep0, s_tlab[ed], x, y, 2, vd > v0);
+        if (v0 + vr == 255) { hm |= 1; n0 = s_tlab[er]; }
+        if (v0 + vdr == 255) { hm |= 2; n1 = s_tlab[edr]; }
+        if (v0 + vd == 255) { hm |= 4; n2 = s_tlab[ed]; }
         const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1;
-        if (!dedup && v0 + vdl == 255) pk[3] = make_qbp(rep0, s_tlab[edl], x, y, 3, vdl > v0);
+        if (!dedup && v0 + vdl == 255) { hm |= 8; n3 = s_tlab[edl]; }
       }
     }
+    const uint32_t nbd[4] = {n0, n1, n2, n3};
+    auto key_of = [&](int dir) { return make_qbp(rep0, nbd[dir], x, y, dir, b2w); };
+    // a direction's pair as the lane sees it (rep0 fixed): the neighbour's side of rep0 and
+    // its 20 key bits -- equal exactly when the directions' 40-bit pair keys are equal
+    auto pid = [&](uint32_t n) { return (n > rep0 ? 0x80000000u : 0u) | (n & 0xfffffu); };
     uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
+#pragma unroll
+    for (int dir = 0; dir < 4; dir++) {
+      const uint64_t hmask = __ballot((hm >> dir) & 1);
+      below += lanes_below(hmask);
+      wtot += (uint32_t)__popcll(hmask);
+    }
     // pair histogram: a pixel's (up to four) points nearly always share one pair,
     // so a lane adds its first pair with the count of its points in it, runs of
     // equal pairs in consecutive lanes sum their counts (wave scan), and only the
     // rare other pairs of a lane go in one by one
-    uint64_t kp = 0;
-    uint32_t cnt = 0;
-    bool got = false;
+    const bool got = hm != 0;
+    const uint32_t nf = (hm & 1) ? n0 : (hm & 2) ? n1 : (hm & 4) ? n2 : n3;  // first direction's neighbour
+    const uint32_t pf = pid(nf);
+    uint32_t cnt = 0, xm = 0;  // points in the first pair; directions of other pairs
 #pragma unroll
     for (int dir = 0; dir < 4; dir++) {
-      const bool has = pk[dir] != 0;
-      const uint64_t hmask = __ballot(has);
-      below += lanes_below(hmask);
-      wtot += (uint32_t)__popcll(hmask);
-      if (has) {
-        const uint64_t r01 = pk[dir] >> 24;
-        if (!got) kp = r01;
-        got = true;
-        cnt += r01 == kp;
-      }
+      const bool in = (hm >> dir) & 1, eq = pid(nbd[dir]) == pf;
+      cnt += in && eq;
+      xm |= (in && !eq) ? 1u << dir : 0u;
     }
+    const uint64_t kp = got ? make_qbp(rep0, nf, 0, 0, 0, false) >> 24 : 0ull;
     {
       const uint64_t prev = wave_shr1_u64(kp);
       const bool same = got && lane > 0 && prev == kp;
@@ -1459,15 +1469,13 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
           s_spill = 1;
         }
       }
-      bool extra = false;
-#pragma unroll
-      for (int dir = 0; dir < 4; dir++) extra |= pk[dir] != 0 && (pk[dir] >> 24) != kp;
-      if (__ballot(extra)) {
+      if (__ballot(xm != 0)) {
 #pragma unroll
         for (int dir = 0; dir < 4; dir++) {
-          if (pk[dir] != 0 && (pk[dir] >> 24) != kp) {
-            if (!lds_pair_add(s_pkey, s_pcnt, pk[dir] >> 24, 1u)) {
-              bnd_spill(b, f, pk[dir] >> 24, 1u);
+          if ((xm >> dir) & 1) {
+            const uint64_t k = key_of(dir) >> 24;
+            if (!lds_pair_add(s_pkey, s_pcnt, k, 1u)) {
+              bnd_spill(b, f, k, 1u);
               s_spill = 1;
             }
           }
@@ -1481,9 +1489,10 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     uint32_t pos = wbase + below;
 #pragma unroll
     for (int dir = 0; dir < 4; dir++)
-      if (pk[dir]) {
-        if (pos < (uint32_t)kBndStage) s_pts[pos] = pk[dir];
-        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = pk[dir];
+      if ((hm >> dir) & 1) {
+        const uint64_t k = key_of(dir);
+        if (pos < (uint32_t)kBndStage) s_pts[pos] = k;
+        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = k;
         else atomicOr(b.status + f, kStatusPointsOverflow);
         pos++;
       }
