@@ -376,7 +376,7 @@ template <int TWD, int PRE>
 __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT_THR_SGPRS))) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
   using CT = CclTile<TWD>;
   constexpr int NT = CT::NT;
-  constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES, kCclRowNodes = CT::ROW_NODES;
+  constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES;
   constexpr int kTW = kCclTileW / 4, kTH = kCclTileH / 4;  // 4x4 threshold tiles per CCL tile
   constexpr int kHR = kCclTileH + 1, kHC = kCclTileW + 2;  // threshold halo: rows y0-1.., cols x0-1..x0+W
   const int f = blockIdx.z;
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
   __shared__ uint16_t s_li[TWD == 64 ? kCclTileNodes : 1];  // list slot of each listed root (border descriptor)
+  __shared__ uint32_t s_gid[kCclTileNodes];  // global node id of every slot (the publish reads its roots')
   if (tid == 0) s_nlr = 0;
   // unfiltered tile min/max for tile rows ty0-2..ty0+kTH, cols tx0-2..tx0+kTW+1
   const int ty0 = y0 / 4, tx0 = x0 / 4;
@@ -649,6 +650,12 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   s_par[F] = rF;
   s_par[L] = rL;
   s_par[R] = rR;
+  // every slot's global node id, by its owner (the publish looks its roots' ids up
+  // instead of decoding slot numbers: ~15 VALU per decode)
+  const uint32_t idF = (uint32_t)(2 * (y0 / 2 + bty) * g.Wd + 2 * (x0 / 2 + btx)), idL = idF + g.Wd;
+  s_gid[F] = idF;
+  s_gid[L] = idL;
+  s_gid[R] = idL + 1;
   const uint32_t nfg = (a == 255) + (bb == 255) + (c == 255) + (d == 255);
   const uint32_t nbl = (a == 0) + (c == 0), nbr = (bb == 0) + (d == 0);
   // components reaching a border block may be merged across tiles (k_ccl_border);
@@ -698,17 +705,9 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   }
   const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
   if (inimg) {
-    auto gid = [&](uint32_t s) -> uint32_t {
-      const int sty = s / kCclRowNodes, r = s % kCclRowNodes;
-      const int gy = y0 / 2 + sty;
-      if (r < kCclBW) return (uint32_t)(2 * gy * g.Wd + 2 * (x0 / 2 + r));
-      const int k = r - kCclBW;
-      return (uint32_t)((2 * gy + 1) * g.Wd + 2 * (x0 / 2 + (k >> 1)) + (k & 1));
-    };
+    auto gid = [&](uint32_t s) -> uint32_t { return s_gid[s]; };
     uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
     uint32_t* size = b.size + (size_t)f * g.Wd * g.Hd;
-    const uint32_t idF = (uint32_t)(2 * BY * g.Wd + 2 * BX);
-    const uint32_t idL = idF + g.Wd;
     // a root of a tile-interior component is final: in throughput mode (k_ccl_merge
     // sets the others' kept bits) its parent word gets the kept bit here and it is not listed
     auto fin = [&](uint32_t w, uint32_t c) -> uint32_t {
@@ -716,9 +715,9 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     };
     uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
     uint32_t* lc = b.lcnt + tl * kCclTileNodesMax;
-    if (lF) { lr[iF] = gid(F); if (!(AT_TC_EXP & 2)) lc[iF] = cF; }
-    if (lL) { lr[iL] = gid(L); if (!(AT_TC_EXP & 2)) lc[iL] = cL; }
-    if (lR) { lr[iR] = gid(R); if (!(AT_TC_EXP & 2)) lc[iR] = cR; }
+    if (lF) { lr[iF] = idF; if (!(AT_TC_EXP & 2)) lc[iF] = cF; }
+    if (lL) { lr[iL] = idL; if (!(AT_TC_EXP & 2)) lc[iL] = cL; }
+    if (lR) { lr[iR] = idL + 1; if (!(AT_TC_EXP & 2)) lc[iR] = cR; }
     // throughput mode: a listed root's own word names its list slot (kListBit | slot)
     // until k_ccl_merge overwrites it with the component's root
     auto word = [&](uint32_t r, uint32_t w, uint32_t c, bool listed, uint32_t li) -> uint32_t {
