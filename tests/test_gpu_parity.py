@@ -482,3 +482,22 @@ def test_ccl_merge_and_fallback_in_one_batch(gpu, oracle_mod):
         orc.detect(f, 2)
         assert compare_frame(det, orc, frame_idx=c) == [], c
         assert compare_detections(res[c], orc.detections()) == [], c
+
+
+def test_ccl_merge_counts_at_l2_1080p(gpu, oracle_mod):
+    """1080p noise frames list ~11 k local roots: more than the 14 B per root of pixel
+    counts fit beside the parent keys in k_ccl_merge's LDS, so the counts are summed in
+    the size plane at L2 (10 B per root) -- no frame may fall back to the global merge,
+    and every stage (labels, sizes, kept bits) stays bit-exact against the oracle."""
+    from ros_vision_amd import synth
+    frames = [synth.stream_frame(1920, 1080, k)[1] for k in (3, 7)]
+    det = gpu.GpuDetector(1920, 1080, max_batch=8)
+    res = det.detect_batch(frames, gpu.AT_FMT_GRAY8)
+    st = det.batch_stats()
+    assert st["ccl_fallback_frames"] == 0, st
+    assert st["ccl_listed_roots_max"] * 14 > 153600, st  # (the counts-at-L2 layout ran)
+    for c, f in enumerate(frames):
+        orc = oracle_mod.Oracle(1920, 1080)
+        orc.detect(f, 2)
+        assert compare_frame(det, orc, frame_idx=c) == [], c
+        assert compare_detections(res[c], orc.detections()) == [], c
