@@ -388,7 +388,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
 
   __shared__ uint8_t s_umn[kTH + 3][kTW + 4], s_umx[kTH + 3][kTW + 4];
   __shared__ uint8_t s_fmn[kTH + 1][kTW + 2], s_fmx[kTH + 1][kTW + 2];
-  __shared__ uint8_t s_t[kHR][kHC + 2];  // thr of rows y0-1..y0+H-1, cols x0-1..x0+W (+pad)
+  __shared__ __attribute__((aligned(4))) uint8_t s_t[kHR][kHC + 2];  // thr of rows y0-1..y0+H-1, cols x0-1..x0+W (+pad)
   __shared__ uint32_t s_par[kCclTileNodes];
   __shared__ uint32_t s_cnt[kCclTileNodes];
   __shared__ uint32_t s_nlr;
@@ -399,6 +399,10 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   const int ty0 = y0 / 4, tx0 = x0 / 4;
   constexpr int kDecPer = (kHR * kHC + NT - 1) / NT;
   uint8_t dv[kDecPer];
+  // PRE < 0: the halo rows as 4-byte windows, window j of row r = cols x0-1+4j .. x0+2+4j
+  // (s_t's dword j of row r), one task per window: 561 tasks instead of 2178 bytes
+  constexpr int kWin = (kHC + 2) / 4, kWinN = kHR * kWin, kWinPer = (kWinN + NT - 1) / NT;
+  uint32_t dw4[kWinPer];
   // PRE: decimated samples of rows y0-8 .. y0+35, cols x0-8 .. x0+TW+7 (the tiles
   // of s_umn), staged over s_par (unused until the labeling)
   constexpr int kDR = kCclTileH + 12, kDC = kCclTileW + 16;
@@ -509,16 +513,17 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     __syncthreads();  // s_dec (over s_par) read before the labeling writes s_par
   } else {
   // the tile's decimated pixels (+1 halo) are loaded together with the tile
-  // min/max: one global round trip instead of two
+  // min/max: one global round trip instead of two.  A window straddles two aligned
+  // dwords of its row (W/2 is a multiple of 4); loads from clamped addresses (no
+  // branch per load), the bytes outside the image are masked by the threshold
+  (void)dv;
 #pragma unroll
-  for (int k = 0; k < kDecPer; k++) {
-    const int i = tid + NT * k;
-    const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
-    // unconditional load from the clamped address, select afterwards: no
-    // branch per load, so all kDecPer loads issue back to back
-    const int yc = min(max(y, 0), g.Hd - 1), xc = min(max(x, 0), g.Wd - 1);
-    const uint8_t v = dec[(size_t)yc * g.Wd + xc];
-    dv[k] = (i < kHR * kHC && y == yc && x == xc) ? v : 0;
+  for (int k = 0; k < kWinPer; k++) {
+    const int t = tid + NT * k, r = t / kWin, j = t % kWin;
+    const int yc = min(max(y0 - 1 + r, 0), g.Hd - 1), wd4 = g.Wd >> 2, xa = (x0 >> 2) + j - 1;
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(dec + (size_t)yc * g.Wd);
+    const uint32_t A = row[min(max(xa, 0), wd4 - 1)], B = row[min(xa + 1, wd4 - 1)];
+    dw4[k] = __builtin_amdgcn_alignbyte(B, A, 3);  // A's last byte, B's first three
   }
   for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
     const int r = i / (kTW + 4), c = i % (kTW + 4);
@@ -549,6 +554,33 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   __syncthreads();
   ph(2);
   // InternalThreshold for the halo region; outside the image -> 127
+  if constexpr (PRE < 0) {
+    // one 4-byte window per task: byte 0 in 4x4 tile column j of the filtered
+    // min/max, bytes 1-3 in column j + 1
+#pragma unroll
+    for (int k = 0; k < kWinPer; k++) {
+      const int t = tid + NT * k, r = t / kWin, j = t % kWin, y = y0 - 1 + r;
+      if (t < kWinN) {
+        uint32_t out = 0x7f7f7f7fu;
+        if (y >= 0 && y < g.Hd) {
+          const int fr = (y >> 2) - (ty0 - 1);
+          const int mn0 = s_fmn[fr][j], mx0 = s_fmx[fr][j], mn1 = s_fmn[fr][j + 1], mx1 = s_fmx[fr][j + 1];
+          const bool ok0 = mx0 - mn0 >= prm.min_white_black_diff, ok1 = mx1 - mn1 >= prm.min_white_black_diff;
+          const uint32_t th0 = (uint32_t)(mn0 + (mx0 - mn0) / 2), th1 = (uint32_t)(mn1 + (mx1 - mn1) / 2);
+          out = 0;
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {
+            const int x = x0 - 1 + 4 * j + bb;
+            const bool ok = bb == 0 ? ok0 : ok1;
+            const uint32_t v = (dw4[k] >> (8 * bb)) & 0xffu, th = bb == 0 ? th0 : th1;
+            const uint32_t res = (x < 0 || x >= g.Wd || !ok) ? 127u : (v > th ? 255u : 0u);
+            out |= res << (8 * bb);
+          }
+        }
+        *reinterpret_cast<uint32_t*>(&s_t[r][4 * j]) = out;
+      }
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < kDecPer; k++) {
     const int i = tid + NT * k;
@@ -568,6 +600,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
       }
       s_t[r][c] = res;
     }
+  }
   }
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
   __syncthreads();
