@@ -2107,6 +2107,19 @@ __device__ __forceinline__ float ext_dot(const Ext& e) {
   return (float)(a - bq + c);
 }
 
+// Line-fit weight of TransformLineFitPoint (apriltag_gpu.cu:631-687): (int)(hypotf(gx, gy)
+// + 1), hypotf being (float)sqrt((double)gx^2 + (double)gy^2) (det_hypotf).  For byte
+// differences (|gx|, |gy| <= 255) that is exactly floor(sqrt(gx^2 + gy^2)) + 1: a
+// non-square s = gx^2 + gy^2 lies >= 1 / 724 below the next integer root, far above the
+// float rounding near 362 (2^-15) -- so an integer square root instead of an fp64 one
+__device__ __forceinline__ int32_t lf_weight(int32_t gx, int32_t gy) {
+  const uint32_t sq = (uint32_t)(gx * gx + gy * gy);
+  uint32_t r = (uint32_t)__builtin_amdgcn_sqrtf((float)sq);  // (v_sqrt_f32: within one of the root)
+  r -= r * r > sq ? 1u : 0u;
+  r += (r + 1) * (r + 1) <= sq ? 1u : 0u;
+  return (int32_t)r + 1;
+}
+
 struct Moments {
   int32_t Mx, My, W;
   int64_t Mxx, Myy, Mxy;
@@ -3008,7 +3021,7 @@ __device__ bool small_extents_keys(const DevBufs& b, const Geom& g, int f, uint3
     if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
       const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
       const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
-      Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+      Wt = lf_weight(gxv, gyv);
     }
     kv[u] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
             ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
@@ -3090,7 +3103,7 @@ __device__ bool large_extents_keys(const DevBufs& b, const Geom& g, BlobShared<N
     if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
       const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
       const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
-      Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+      Wt = lf_weight(gxv, gyv);
     }
     kv[u] = ((uint64_t)(ti & 0xfffffff) << kKeyTheta) | ((uint64_t)dxy << 30) | ((uint64_t)by << 20) |
             ((uint64_t)bx << 10) | (((k >> 3) & 1) << 9) | (uint64_t)Wt;
@@ -3753,7 +3766,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
       if (ix > 0 && ix + 1 < g.Wd && iy > 0 && iy + 1 < g.Hd) {
         const int32_t gxv = (int32_t)((gp[u] >> 8) & 0xff) - (int32_t)(gp[u] & 0xff);
         const int32_t gyv = (int32_t)(gp[u] >> 24) - (int32_t)((gp[u] >> 16) & 0xff);
-        Wt = (int32_t)(det_hypotf((float)gxv, (float)gyv) + 1.0f);
+        Wt = lf_weight(gxv, gyv);
       }
       // sort key: order (theta, plane, y, x) == P6 stable order; b2w and W ride in
       // the low bits (never decide: (plane, y, x) is unique)

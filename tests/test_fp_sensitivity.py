@@ -51,3 +51,18 @@ def test_faithful_libm_keeps_integer_outputs(committed):
         assert tot[cname]["det_integer_corner_changes"] == 0, cname
         assert tot[cname]["det_corner_max_px"] < 2.5e-4, cname  # <= 2 float ulps at x < 2048
         assert tot[cname]["theta_order"] <= 1e-4 * tot["index_points"], cname
+
+
+def test_line_fit_weight_is_integer_sqrt_plus_one():
+    """k_extents / the fused blob paths compute TransformLineFitPoint's weight
+    (int)(hypotf(gx, gy) + 1) -- hypotf as (float)sqrt((double)gx^2 + (double)gy^2), the
+    oracle's det_hypotf -- as floor(sqrt(gx^2 + gy^2)) + 1 with an integer square root
+    (lf_weight, at_kernels.hip).  Exhaustive over the byte differences the gradient takes."""
+    import numpy as np
+    g = np.arange(-255, 256, dtype=np.int64)
+    s = (g[:, None] ** 2 + g[None, :] ** 2).ravel()
+    ref = np.trunc(np.sqrt(s.astype(np.float64)).astype(np.float32) + np.float32(1.0)).astype(np.int64)
+    r = np.floor(np.sqrt(s.astype(np.float64))).astype(np.int64)
+    r -= (r * r > s)
+    r += ((r + 1) * (r + 1) <= s)
+    assert np.array_equal(ref, r + 1)
