@@ -2445,12 +2445,15 @@ __device__ __forceinline__ Moments to_moments(const Mom6& s, int32_t N) {
 // evaluates it (float result)
 __device__ __forceinline__ float window_err(const Mom6& s, int32_t N) {
   const Moments m = to_moments(s, N);
-  const int64_t Wl = m.W;
-  const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
-  const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
-  const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
+  // a window's weight sum is below 2^14 (at most 41 points of weight <= 362): 64 x 32-bit
+  // products, and 8 W^2 < 2^32 converts exactly as an unsigned int (the double product the
+  // reference rounds to float is the same integer)
+  const uint64_t Wl = (uint32_t)m.W;
+  const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
+  const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
+  const int64_t Cyy = (int64_t)((uint64_t)m.Myy * Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
   const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
-  const float eig = ((float)(Cxx + Cyy) - h) / (float)((double)(Wl * Wl) * 8.0);
+  const float eig = ((float)(Cxx + Cyy) - h) / (float)(8u * (uint32_t)Wl * (uint32_t)Wl);
   return (float)m.N * eig;
 }
 
