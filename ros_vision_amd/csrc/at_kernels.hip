@@ -363,9 +363,6 @@ constexpr uint32_t kTouchBit = 0x80000000u;
 #ifndef AT_THR_SGPRS
 #define AT_THR_SGPRS 80
 #endif
-#ifndef AT_TC_EXP
-#define AT_TC_EXP 0  // (cost attribution builds only)
-#endif
 // PRE < 0: the tile's decimated pixels and 4x4 min/max come from k_pre's planes.
 // PRE = 0 / 1 / 2 (frame format YUYV / BGR8 / GRAY8): k_pre's work is done here --
 // the workgroup reads its tile's full-resolution rows once (gray and decimated
@@ -730,7 +727,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
                  iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
   constexpr bool kKeep = TWD != 32;
-  if constexpr (kKeep && !(AT_TC_EXP & 4)) {  // list slots of the roots, for the border descriptor
+  if constexpr (kKeep) {  // list slots of the roots, for the border descriptor
     if (lF) s_li[F] = (uint16_t)iF;
     if (lL) s_li[L] = (uint16_t)iL;
     if (lR) s_li[R] = (uint16_t)iR;
@@ -748,9 +745,9 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     };
     uint32_t* lr = b.lroot + tl * kCclTileNodesMax;
     uint32_t* lc = b.lcnt + tl * kCclTileNodesMax;
-    if (lF) { lr[iF] = idF; if (!(AT_TC_EXP & 2)) lc[iF] = cF; }
-    if (lL) { lr[iL] = idL; if (!(AT_TC_EXP & 2)) lc[iL] = cL; }
-    if (lR) { lr[iR] = idL + 1; if (!(AT_TC_EXP & 2)) lc[iR] = cR; }
+    if (lF) { lr[iF] = idF; lc[iF] = cF; }
+    if (lL) { lr[iL] = idL; lc[iL] = cL; }
+    if (lR) { lr[iR] = idL + 1; lc[iR] = cR; }
     // throughput mode: a listed root's own word names its list slot (kListBit | slot)
     // until k_ccl_merge overwrites it with the component's root
     auto word = [&](uint32_t r, uint32_t w, uint32_t c, bool listed, uint32_t li) -> uint32_t {
@@ -765,7 +762,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
       else size[idL + 1] = cR;
     }
   }
-  if constexpr (TWD == 64 && !(AT_TC_EXP & 1)) {
+  if constexpr (TWD == 64) {
     // throughput mode: the tile's border descriptor for k_ccl_merge (CclDesc) --
     // the threshold bytes of its outer rows / columns and the list slots of the
     // roots of its border blocks' nodes (a node with pixels in a border block
@@ -776,7 +773,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     // whole-word stores: a wave holds two block rows, so the slots of blocks (x, x+1)
     // of a row are in lanes l, l+1 and those of block rows (2i, 2i+1) of a column in
     // lanes l, l+32 of wave i
-    if (!(AT_TC_EXP & 8)) {
+    {
     const uint32_t sF = nfg ? s_li[rF] : 0xffffu, sL = nbl ? s_li[rL] : 0xffffu, sR = nbr ? s_li[rR] : 0xffffu;
     const uint32_t nF = wave_read_next(sF), nL = wave_read_next(sL), nR = wave_read_next(sR);
     const int w = tid >> 6;
@@ -801,8 +798,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     auto row4 = [&](int r, int c) -> uint32_t {  // (byte reads: the rows start at odd offsets)
       return s_t[r][c] | (s_t[r][c + 1] << 8) | (s_t[r][c + 2] << 16) | ((uint32_t)s_t[r][c + 3] << 24);
     };
-    if (AT_TC_EXP & 16) {
-    } else if (tid < 16) {
+    if (tid < 16) {
       dw[CclDesc::Tthr + tid] = row4(1, 1 + 4 * tid);
     } else if (tid < 32) {
       dw[CclDesc::Bthr + tid - 16] = row4(kCclTileH, 1 + 4 * (tid - 16));
@@ -1403,25 +1399,25 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   // the byte then picks fg or bg: one round trip fewer than thr -> node -> parent)
   uint32_t lv[kPer], lb[kPer];
   uint8_t tv[kPer];
+  // loads from clamped addresses, selected afterwards (no branch per load)
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     const int e = tid + 256 * k;
     const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
-    lv[k] = 0xffffffffu;
-    lb[k] = 0xffffffffu;
-    tv[k] = 127;
-    if (e < kTN && yy < g.Hd && xx < Wd) {
-      const size_t i = (size_t)yy * Wd + xx;
-      tv[k] = thr[i];
-      const uint32_t F = (uint32_t)((yy & ~1) * Wd + (xx & ~1));
-      lv[k] = par[F];
-      lb[k] = par[F + Wd + (xx & 1)];
-    }
+    const bool in = e < kTN && yy < g.Hd && xx < Wd;
+    const int yc = min(yy, g.Hd - 1), xc = min(xx, Wd - 1);
+    const uint32_t F = (uint32_t)((yc & ~1) * Wd + (xc & ~1));
+    const uint8_t t = thr[(size_t)yc * Wd + xc];
+    const uint32_t a = par[F], c = par[F + Wd + (xc & 1)];
+    tv[k] = in ? t : (uint8_t)127;
+    lv[k] = in ? a : 0xffffffffu;
+    lb[k] = in ? c : 0xffffffffu;
   }
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
     lv[k] = tv[k] == 127 ? 0xffffffffu : (tv[k] == 255 ? lv[k] : lb[k]);
-    if (lv[k] != 0xffffffffu) lv[k] = par[lv[k] & ~kKeptBit];
+    const uint32_t r = par[lv[k] != 0xffffffffu ? (lv[k] & ~kKeptBit) : 0u];
+    lv[k] = lv[k] != 0xffffffffu ? r : 0xffffffffu;
   }
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
@@ -2452,8 +2448,11 @@ __device__ __forceinline__ float window_err(const Mom6& s, int32_t N) {
   const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
   const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * Wl - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
   const int64_t Cyy = (int64_t)((uint64_t)m.Myy * Wl - (uint64_t)((int64_t)m.My * (int64_t)m.My));
-  const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
-  const float eig = ((float)(Cxx + Cyy) - h) / (float)(8u * (uint32_t)Wl * (uint32_t)Wl);
+  // the three int64 -> float conversions through double: |values| < 2^51 here (a window's
+  // second moments), so the double is exact and the one rounding is the direct cast's
+  auto tof = [](int64_t v) { return (float)(double)v; };
+  const float h = det_hypotf(tof(Cxx - Cyy), tof(2 * Cxy));
+  const float eig = (tof(Cxx + Cyy) - h) / (float)(8u * (uint32_t)Wl * (uint32_t)Wl);
   return (float)m.N * eig;
 }
 
