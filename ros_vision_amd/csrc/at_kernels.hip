@@ -1402,8 +1402,8 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   // loads from clamped addresses, selected afterwards (no branch per load)
 #pragma unroll
   for (int k = 0; k < kPer; k++) {
-    const int e = tid + 256 * k;
-    const int yy = ty0 + e / kTC, xx = tx0 + e % kTC;
+    const int e = tid + 256 * k, ec = min(e, kTN - 1);  // (lanes past the tile read its last element)
+    const int yy = ty0 + ec / kTC, xx = tx0 + ec % kTC;
     const bool in = e < kTN && yy < g.Hd && xx < Wd;
     const int yc = min(yy, g.Hd - 1), xc = min(xx, Wd - 1);
     const uint32_t F = (uint32_t)((yc & ~1) * Wd + (xc & ~1));
