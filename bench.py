@@ -43,7 +43,9 @@ DOMINANT = "k_thr_ccl"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
+    """The bench's options; parse([]) gives the headline defaults (the parity test of the
+    headline configuration, tests/test_stream_parity.py, takes them from here)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
@@ -74,6 +76,12 @@ def parse():
     ap.add_argument("--node-path-calls", type=int, default=300,
                     help="the deployed node's per-frame path, B=1: DetectorCore::process on bgr8 host frames "
                          "at 1920x1080 and 800x600 (node/at_mock_node --time), p50/p99 per call; 0 = skip")
+    ap.add_argument("--isolated-batches", type=int, default=10,
+                    help="batches per kernel of the isolated roofline pass (one batch in flight, each kernel of "
+                         "the sequence timed on its own stream in turn); 0 = skip")
+    ap.add_argument("--isolated-only", action="store_true",
+                    help="only the isolated roofline pass (no concurrent loop): the command profiled by "
+                         "rocprofv3 --kernel-trace for profiles/, every launch in the process serialized")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-profile", action="store_true")
     ap.add_argument("--timed-kernel", default=None,
@@ -115,6 +123,58 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_pose":  # per candidate detection: H + corners in, R, t, errors out
         return stats.get("candidates", 0) * (72 + 64 + 112)
     return None
+
+
+def isolated_kernel_times(det, batch_ptr, stride, B, nbatches):
+    """Every kernel of the launch sequence on its own: one batch in flight (enqueue,
+    collect), the kernel timer on one kernel at a time (the sequence as three graphs
+    cut around it), two warm-up batches, then `nbatches` timed.  {kernel: (device-clock
+    span ms, HIP-event ms, launches, batch stats)} -- the kernel's duration when it
+    has the chip, which a rocprofv3 kernel trace reproduces (tracing does not change
+    a serialized launch; it does change how concurrent batches interleave)."""
+    from ros_vision_amd import detector
+    L = detector.load_library()
+    names = []
+    for i in range(32):
+        nm = L.at_stage_name(i)
+        if not nm:
+            break
+        names.append(nm.decode())
+    out = {}
+    s = 0
+    for k in names:
+        try:
+            det.set_kernel_timer(k)
+        except Exception:
+            continue
+        for _ in range(2):
+            det.enqueue_device(batch_ptr(s), stride, B)
+            det.collect(counts_only=True)
+            s += 1
+        det.set_kernel_timer(k)  # reset the accumulators
+        for _ in range(nbatches):
+            det.enqueue_device(batch_ptr(s), stride, B)
+            det.collect(counts_only=True)
+            s += 1
+        span, nspan = det.kernel_span()
+        ev, nev = det.kernel_time()
+        if nspan > 0 and span > 0:
+            out[k] = (span, ev, nspan, det.batch_stats())
+    det.set_kernel_timer(None)
+    return out
+
+
+def isolated_table(iso, W, H):
+    """isolated_kernel_times -> [{kernel, ms, algorithmic bytes, achieved, frac}], longest first."""
+    rows = []
+    for k, (span, ev, n, st) in sorted(iso.items(), key=lambda kv: -kv[1][0]):
+        kb = kernel_algorithmic_bytes(k, st, W, H)
+        gbs = kb / (span * 1e-3) / 1e9 if kb else None
+        rows.append({"kernel": k, "avg_launch_ms_device_clock": round(span, 5), "avg_launch_ms_hip_events": round(ev, 5),
+                     "launches": n, "algorithmic_bytes_per_launch": kb,
+                     "achieved": round(gbs, 3) if gbs else None,
+                     "frac": round(gbs / HBM_PEAK_GBS, 6) if gbs else None})
+    return rows
 
 
 def pmc_traffic(W, H):
@@ -244,9 +304,7 @@ def main():
     W, H, B = args.width, args.height, args.batch
     scatter = args.ingest == "scatter"
     frames = render_pool(args, rank)
-    # scatter: rank 0's pool per rank holds at least one batch (the pool repeated)
-    copies = -(-B // args.pool) if scatter else (max(1, args.hbm_copies) if args.hbm_copies
-                                                  else max(4, -(-2 * B // args.pool)))
+    copies = pool_copies(args)
     d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
     stride = frames[0].nbytes
     base = d_frames.data_ptr()
@@ -262,23 +320,26 @@ def main():
             for r in range(world):
                 root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames).repeat(copies, 1, 1)
         ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
-        rec_cap = 32  # detection records per frame gathered to rank 0 (fixed capacity)
+        rec_cap = 32  # detection records per frame in the fixed-size message; more follow in the overflow one
         rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)
         copied = {}  # detector -> event after the async copy out of its pinned buffer
         gather = multigpu.RecordGather(dist, B, rec_bytes, "cuda")
 
     def gather_results(d, s):
-        """Fixed-capacity detection records of the other ranks' batches -> rank 0
-        (multigpu.RecordGather: RCCL point-to-point).  at_collect wrote them into
-        pinned host memory, read by an async copy; rank 0's own stay there, at world
-        size 1 nothing moves."""
+        """Every detection record of the other ranks' batches -> rank 0
+        (multigpu.RecordGather: RCCL point-to-point): a fixed-size row of the first
+        rec_cap records per frame with the frame's true count, read from the pinned
+        buffer at_collect wrote by an async copy, plus an overflow message with the
+        records past rec_cap of the frames that have more.  Rank 0's own stay in its
+        host buffer; at world size 1 nothing moves."""
         if world == 1:
             return
         if rank == 0:
             gather.post(s)
         else:
-            gather.post(s, d._out_t.view(B, -1)[:, :rec_bytes],
-                        torch.tensor([min(d._n[f], rec_cap) for f in range(B)], dtype=torch.int32))
+            counts = [d._n[f] for f in range(B)]
+            gather.post(s, d._out_t.view(B, -1)[:, :rec_bytes], torch.tensor(counts, dtype=torch.int32),
+                        multigpu.overflow_from(counts, rec_cap, d.frame_record_bytes))
             copied[id(d)] = gather.copied[s % 2]
 
     runner = StreamRunner(dets, base, stride, npool, B)
@@ -326,6 +387,16 @@ def main():
         ingest.drain()
         return ndet
 
+    if args.isolated_only:  # (the rocprofv3 command of profiles/: every launch serialized)
+        iso = isolated_kernel_times(dets[0], batch_ptr, stride, B, max(1, args.isolated_batches))
+        if rank == 0:
+            print(json.dumps({"mode": "isolated-only", "batch": B, "width": W, "height": H,
+                              "isolated": isolated_table(iso, W, H)}), file=json_out, flush=True)
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
     run(max(1, args.warmup))
 
     # per-stage GPU time (HIP events between the kernels, serialized launch
@@ -354,6 +425,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host0 = [d.batch_stats() for d in dets]
+    gathered0 = gather.records_received if scatter else 0
     ndet = run(args.steps, step0=args.warmup)
     torch.cuda.synchronize()
     if dist.is_initialized():
@@ -371,6 +443,9 @@ def main():
     # reports); the HIP-event bracket also holds the launch's wait for free CUs
     # behind the other batches in flight
     k_ms = k_ms_span if k_spans else k_ms_events
+    # scatter: the detection records rank 0 holds after the timed region (its own + every
+    # peer's, overflow included) -- equal to the detections of all ranks
+    records_at_root = (ndet + gather.records_received - gathered0) if (scatter and rank == 0) else None
     stats = dets[0].batch_stats()
     for d in dets:
         d.set_kernel_timer(None)
@@ -383,6 +458,11 @@ def main():
         ndet = int(nd.item())
     total_frames = world * args.steps * B
     fps = total_frames / elapsed
+
+    # every kernel on its own (one batch in flight): the headline roofline kernel is
+    # the one with the longest isolated launch
+    iso = isolated_kernel_times(dets[0], batch_ptr, stride, B, args.isolated_batches) \
+        if (args.isolated_batches > 0 and not args.no_kernel_timer) else {}
 
     # per-frame latency, one frame at a time (B = 1), detections in host memory:
     # from a (pageable) host frame as the node feeds it, and from
@@ -450,25 +530,55 @@ def main():
 
     per_gpu_fps = fps / world
     pipe_ms = sum(stages.values()) if stages else None
-    kbytes = kernel_algorithmic_bytes(dominant, stats, W, H)
     pmc = pmc_traffic(W, H)
-    k_traffic = None
-    if pmc and dominant:
-        kk = [v for k, v in pmc.get("kernels", {}).items() if k.split("<")[0] == dominant]
-        if kk:  # FETCH x2 (gfx950 correction) + WRITE, per frame -> per launch
-            k_traffic = round(B * sum(2 * v["fetch_bytes_per_frame"] + v["write_bytes_per_frame"] for v in kk))
+
+    def traffic_per_launch(kernel):
+        """PMC bytes of one launch of `kernel` (FETCH x2 (gfx950 correction) + WRITE per
+        frame, profiles/pmc_traffic.json, x the batch)."""
+        kk = [v for k, v in (pmc or {}).get("kernels", {}).items() if k.split("<")[0] == kernel]
+        return round(B * sum(2 * v["fetch_bytes_per_frame"] + v["write_bytes_per_frame"] for v in kk)) if kk else None
+
+    # headline roofline: the kernel with the longest isolated launch (one batch in
+    # flight), its device-clock span in this run
+    iso_rows = isolated_table(iso, W, H)
+    head = iso_rows[0] if iso_rows else None
+    # concurrent: the DOMINANT kernel timed inside the timed region (four batches in flight)
+    kbytes = kernel_algorithmic_bytes(dominant, stats, W, H)
     k_achieved = kbytes / (k_ms * 1e-3) / 1e9 if (kbytes and k_ms > 0) else None
     pipe_bytes = 3 * W * H  # SURVEY.md 8(d): read YUYV 2WH + write gray WH
-    # the three largest serialized stages on their own (stage profile: HIP events
-    # between the kernels of one batch in flight): algorithmic bytes / stage time
-    isolated = []
-    for kname in sorted(stages, key=stages.get, reverse=True)[:3]:
-        kb = kernel_algorithmic_bytes(kname, stats, W, H)
-        ms = stages[kname]
-        gbs = kb / (ms * 1e-3) / 1e9 if (kb and ms > 0) else None
-        isolated.append({"kernel": kname, "ms_per_batch": round(ms, 4), "algorithmic_bytes_per_launch": kb,
-                         "achieved": round(gbs, 3) if gbs else None,
-                         "frac": round(gbs / HBM_PEAK_GBS, 6) if gbs else None})
+    top_stage = max(stages, key=stages.get) if stages else None
+    if head:
+        roofline = {"bound": "hbm", "kernel": head["kernel"], "achieved": head["achieved"], "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": head["frac"], "traffic": traffic_per_launch(head["kernel"]),
+                    "algorithmic_bytes_per_launch": head["algorithmic_bytes_per_launch"],
+                    "avg_launch_ms": head["avg_launch_ms_device_clock"],
+                    "avg_launch_ms_hip_events": head["avg_launch_ms_hip_events"], "launches_timed": head["launches"],
+                    "isolated": iso_rows,
+                    "note": "the launch sequence's longest kernel, measured in isolation in this run: one batch of "
+                            "%d frames in flight (enqueue, collect), the kernel timer on one kernel at a time, "
+                            "avg_launch_ms = its execution span on the device wall clock (first workgroup start "
+                            "to last workgroup end, at_kernel_span: what a rocprofv3 kernel trace reports; "
+                            "`bench.py --isolated-only` under rocprofv3 --kernel-trace reproduces it, "
+                            "profiles/); algorithmic bytes per DESIGN.md section 4; traffic = PMC "
+                            "(2*FETCH_SIZE+WRITE_SIZE) per launch from profiles/pmc_traffic.json; `isolated`: "
+                            "every kernel the same way" % B}
+    else:
+        roofline = None
+    roofline_concurrent = {
+        "bound": "hbm", "kernel": dominant, "achieved": round(k_achieved, 3) if k_achieved else None,
+        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(k_achieved / HBM_PEAK_GBS, 6) if k_achieved else None,
+        "traffic": traffic_per_launch(dominant), "algorithmic_bytes_per_launch": kbytes,
+        "avg_launch_ms": round(k_ms, 5), "launches_timed": k_launches,
+        "avg_launch_ms_device_clock": round(k_ms_span, 5), "launches_device_clock": k_spans,
+        "avg_launch_ms_hip_events": round(k_ms_events, 5),
+        "frac_hip_events": round(kbytes / (k_ms_events * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+        if (kbytes and k_ms_events > 0) else None,
+        "top_serialized_stage": top_stage, "differs_from_top_serialized_stage": bool(top_stage and top_stage != dominant),
+        "note": "DOMINANT (fixed rule: the largest marginal cost in the concurrent loop, profiles/r04c/ablation.txt) "
+                "timed on every launch of the timed region with %d batches in flight: its span there holds the "
+                "other batches' kernels sharing the CUs (co-residency), and a tracer changes how the batches "
+                "interleave, so this figure is not reproducible under rocprofv3; top_serialized_stage = the "
+                "largest stage of this run's stage profile" % args.instances}
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -503,24 +613,9 @@ def main():
         "latency_c3_note": "config C3: one batch of 4 camera frames (pageable host YUYV) -> detections + poses",
         "host_ingest": host_ingest,
         "detections_per_frame": round(ndet / total_frames, 3),
-        "roofline": {"bound": "hbm", "kernel": dominant,
-                     "achieved": round(k_achieved, 3) if k_achieved else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(k_achieved / HBM_PEAK_GBS, 6) if k_achieved else None,
-                     "traffic": k_traffic, "algorithmic_bytes_per_launch": kbytes,
-                     "avg_launch_ms": round(k_ms, 5), "launches_timed": k_launches,
-                     "avg_launch_ms_device_clock": round(k_ms_span, 5), "launches_device_clock": k_spans,
-                     "avg_launch_ms_hip_events": round(k_ms_events, 5),
-                     "frac_hip_events": round(kbytes / (k_ms_events * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
-                     if (kbytes and k_ms_events > 0) else None,
-                     "isolated_top3": isolated,
-                     "note": "kernel named by a fixed rule (DOMINANT: the largest marginal cost in the concurrent "
-                             "loop, profiles/r04c/ablation.txt), timed in the timed region on every launch: "
-                             "avg_launch_ms = its execution span on the device wall clock (first workgroup "
-                             "start to last workgroup end, at_kernel_span; what rocprofv3 --kernel-trace "
-                             "reports), avg_launch_ms_hip_events = HIP events around it on its stream (adds "
-                             "the launch's wait for CUs behind the other batches in flight); algorithmic "
-                             "bytes per DESIGN.md section 4; traffic = PMC (2*FETCH_SIZE+WRITE_SIZE) per "
-                             "launch from profiles/pmc_traffic.json"},
+        "records_at_rank0": records_at_root,
+        "roofline": roofline,
+        "roofline_concurrent": roofline_concurrent,
         "roofline_pipeline": {"bound": "hbm", "achieved": round(per_gpu_fps * pipe_bytes / 1e9, 3),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(per_gpu_fps * pipe_bytes / 1e9 / HBM_PEAK_GBS, 6),

@@ -108,6 +108,11 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> all((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
   const int nframes = (int)(all.size() / fb);
   if (count < 0 || count > nframes) count = nframes;
+  if (time_n > 0 && count <= 0) {  // the timed loop walks the frames modulo count
+    std::fprintf(stderr, "%s: --time needs at least one frame (--count %d, %d frames in %s)\n", argv[0], count,
+                 nframes, frames_path.c_str());
+    return 2;
+  }
   // applyCpuPinningAndScheduling (:601-605): failures are logged, not fatal
   std::string sched_log;
   const bool sched_ok = at_node::apply_cpu_pinning_and_scheduling(prm.pin_to_core, prm.priority, &sched_log);

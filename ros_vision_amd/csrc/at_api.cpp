@@ -760,6 +760,11 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
   // already in the host mirror; a frame with more is copied from HBM)
   const int nf = d->last_nframes;
   int* cnt = d->res_n.data();
+  // a failed copy leaves no stale counts: every frame reads empty until it is done
+  for (int f = 0; f < nf; f++) {
+    cnt[f] = 0;
+    if (n_per_frame) n_per_frame[f] = 0;
+  }
   for (int f = 0; f < nf; f++) {
     const uint32_t status = d->h_ctrl[kCtlStatus * B + f];
     const int ncand = (int)std::min<uint32_t>(d->h_ctrl[kCtlNdets * B + f], kMaxDets);
@@ -773,8 +778,11 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
       if (ncand > kDetPoolPerFrame) {
         std::vector<DevDetection>& v = d->res_ovf[f];
         v.resize(ncand);
-        HIPCHK(hipMemcpy(v.data(), d->d.dets + (size_t)f * kMaxDets, ncand * sizeof(DevDetection),
-                         hipMemcpyDeviceToHost));
+        // on the detector's own (non-blocking) stream: a copy on the null stream would
+        // serialize with every blocking stream of the process (torch's default stream)
+        HIPCHK(hipMemcpyAsync(v.data(), d->d.dets + (size_t)f * kMaxDets, ncand * sizeof(DevDetection),
+                              hipMemcpyDeviceToHost, d->st));
+        HIPCHK(hipStreamSynchronize(d->st));
         cand = v.data();
       }
       d->res_base[f] = cand;

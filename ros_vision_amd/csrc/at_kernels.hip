@@ -4849,11 +4849,14 @@ hipError_t launch_draw(const DrawPrim* prims, int n, uint32_t* last, uint8_t* bg
 
 static size_t merge_lds_bytes(const Geom& g) { return (size_t)g.merge_lds; }
 
-// one-time kernel attributes: k_ccl_merge's dynamic LDS beyond the default limit
+// one-time kernel attributes: k_ccl_merge's dynamic LDS beyond the default limit.  The
+// attribute belongs to the function for the whole process, so it is set to the largest
+// size any geometry launches with (never to this detector's: a later, smaller detector
+// would lower the limit below an earlier, larger one's launches)
 hipError_t prepare_kernels(const Geom& g) {
   if (!g.merge_cap) return hipSuccess;
   return hipFuncSetAttribute((const void*)k_ccl_merge<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)merge_lds_bytes(g));
+                             kMergeLdsMax);
 }
 
 hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, int B, int fmt, int nblobwg,

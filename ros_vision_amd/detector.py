@@ -313,6 +313,11 @@ class GpuDetector:
         got = _check(load_library().at_detections(self._h, f, buf, n), "at_detections")
         return list(buf[:got])
 
+    def frame_record_bytes(self, f):
+        """Every at_detection record of frame f of the last batch, as bytes (what a peer
+        sends rank 0, multigpu.RecordGather)."""
+        return b"".join(bytes(r) for r in self._frame_records(f))
+
     def _unpack(self, nframes):
         res = []
         for f in range(nframes):

@@ -9,14 +9,13 @@ exchange between frames.  Two modes:
   rank 0, which sends each other rank its fixed-size YUYV slots (``ScatterIngest``:
   RCCL point-to-point sends over xGMI with backend "nccl", one peer per link;
   ``scatter_frames``: torch.distributed.scatter; gloo on CPU), each rank detects,
-  and ``gather_detections`` returns fixed-capacity detection records to rank 0.
+  and ``RecordGather`` returns every detection record to rank 0 (a fixed-capacity
+  row per frame plus an overflow message for frames with more).
 
 The helpers are backend-agnostic (CPU tensors + gloo in the tests, HBM
 tensors + RCCL on the node).
 """
 import numpy as np
-
-REC = 22  # id, hamming, margin, H[9], c[2], p[4][2]
 
 
 def shard_range(rank: int, world: int, nframes: int):
@@ -24,31 +23,6 @@ def shard_range(rank: int, world: int, nframes: int):
     per = (nframes + world - 1) // world
     lo = min(nframes, rank * per)
     return lo, min(nframes, lo + per)
-
-
-def pack_detections(dets_per_frame, cap: int) -> np.ndarray:
-    """[nframes, cap + 1, REC] float64; row 0 holds the count."""
-    out = np.zeros((len(dets_per_frame), cap + 1, REC), np.float64)
-    for f, dets in enumerate(dets_per_frame):
-        out[f, 0, 0] = min(len(dets), cap)
-        for i, d in enumerate(dets[:cap]):
-            get = (lambda k: d[k]) if isinstance(d, dict) else (lambda k: getattr(d, k))
-            out[f, i + 1, 0] = get("id")
-            out[f, i + 1, 1] = get("hamming")
-            out[f, i + 1, 2] = get("decision_margin")
-            out[f, i + 1, 3:12] = np.asarray(get("H"), np.float64).ravel()
-            out[f, i + 1, 12:14] = np.asarray(get("c"), np.float64)
-            out[f, i + 1, 14:22] = np.asarray(get("p"), np.float64).ravel()
-    return out
-
-
-def unpack_detections(arr: np.ndarray):
-    res = []
-    for f in range(arr.shape[0]):
-        n = int(arr[f, 0, 0])
-        res.append([dict(id=int(r[0]), hamming=int(r[1]), decision_margin=float(r[2]), H=r[3:12].reshape(3, 3),
-                         c=r[12:14].copy(), p=r[14:22].reshape(4, 2)) for r in arr[f, 1:n + 1]])
-    return res
 
 
 def scatter_frames(dist, frames_on_root, frames_per_rank: int, frame_shape, device, dtype=None):
@@ -60,18 +34,6 @@ def scatter_frames(dist, frames_on_root, frames_per_rank: int, frame_shape, devi
     chunks = list(frames_on_root.chunk(world, dim=0)) if rank == 0 else None
     dist.scatter(out, scatter_list=chunks, src=0)
     return out
-
-
-def gather_detections(dist, packed: np.ndarray, device):
-    """Every rank's packed [frames_per_rank, cap+1, REC] records -> rank 0 (list per rank)."""
-    import torch
-    world, rank = dist.get_world_size(), dist.get_rank()
-    t = torch.from_numpy(packed).to(device)
-    gl = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
-    dist.gather(t, gather_list=gl, dst=0)
-    if rank != 0:
-        return None
-    return np.concatenate([g.cpu().numpy() for g in gl], axis=0)
 
 
 class ScatterIngest:
@@ -149,23 +111,124 @@ class ScatterIngest:
         self.work = [None] * self.nbuf
 
 
-class RecordGather:
-    """Fixed-capacity detection records of every rank's batch -> rank 0 (north-star
-    topology): one point-to-point receive per peer on rank 0, one send on each peer
-    (RCCL with backend "nccl", gloo on CPU), double-buffered so the transfer of step
-    s overlaps the detection of the next steps.  Rank 0's own records never move
-    (they are already in its host buffer), so at world size 1 nothing is sent.
+def _rec_size():
+    import ctypes
+    from .detector import AtDetection
+    return ctypes.sizeof(AtDetection)
 
-    A peer's ``post(step, records, counts)``: `records` [batch, rec_bytes] and
-    `counts` [batch] int32 (host tensors; `records` page-locked, read by an async
-    copy -- the caller keeps it intact until ``copied`` of that step has completed);
-    rank 0's ``post(step)`` posts the receives and ``result(step)`` returns the
-    peers' [batch, 4 + rec_bytes] tensors (count, records) once they have arrived."""
+
+def detection_records(dets) -> bytes:
+    """at_detection records (include/at_api.h) of a list of detections (dicts with the
+    oracle's keys or Detection objects), as the C ABI lays them out."""
+    from .detector import AtDetection
+    arr = (AtDetection * max(1, len(dets)))()
+    for i, d in enumerate(dets):
+        get = (lambda k: d[k]) if isinstance(d, dict) else (lambda k: getattr(d, k))
+        arr[i].id, arr[i].hamming, arr[i].decision_margin = int(get("id")), int(get("hamming")), \
+            float(get("decision_margin"))
+        arr[i].H[:] = [float(x) for x in np.asarray(get("H"), np.float64).ravel()]
+        arr[i].c[:] = [float(x) for x in np.asarray(get("c"), np.float64).ravel()]
+        p = np.asarray(get("p"), np.float64).reshape(4, 2)
+        for k in range(4):
+            arr[i].p[k][0], arr[i].p[k][1] = float(p[k, 0]), float(p[k, 1])
+    return bytes(arr)[:len(dets) * _rec_size()]
+
+
+def records_to_dicts(buf) -> list:
+    """Inverse of detection_records: at_detection bytes -> detections as dicts."""
+    from .detector import AtDetection
+    rs = _rec_size()
+    buf = bytes(buf)
+    out = []
+    for i in range(len(buf) // rs):
+        r = AtDetection.from_buffer_copy(buf[i * rs:(i + 1) * rs])
+        out.append(dict(id=r.id, hamming=r.hamming, decision_margin=r.decision_margin,
+                        H=np.array(list(r.H)).reshape(3, 3), c=np.array(list(r.c)),
+                        p=np.array([[r.p[k][0], r.p[k][1]] for k in range(4)])))
+    return out
+
+
+def overflow_from(counts, cap: int, frame_records) -> np.ndarray:
+    """The records past `cap` of every frame that has more, in frame order (uint8,
+    possibly empty); frame_records(f) gives frame f's full at_detection bytes and is
+    called only for those frames."""
+    rs = _rec_size()
+    over = [bytes(frame_records(f))[cap * rs:int(n) * rs] for f, n in enumerate(counts) if n > cap]
+    return np.frombuffer(b"".join(over), np.uint8).copy()
+
+
+def split_records(frame_records, cap: int):
+    """Per-frame at_detection bytes -> what a peer sends rank 0 for one batch: the
+    fixed-capacity rows [nframes, cap * rec] (the first `cap` records of each frame),
+    the TRUE counts [nframes] int32 and the overflow (overflow_from).  Nothing is
+    dropped: join_records restores every frame's full list."""
+    rs = _rec_size()
+    nf = len(frame_records)
+    rows = np.zeros((nf, cap * rs), np.uint8)
+    counts = np.zeros(nf, np.int32)
+    for f, b in enumerate(frame_records):
+        b = bytes(b)
+        counts[f] = len(b) // rs
+        head = b[:min(int(counts[f]), cap) * rs]
+        rows[f, :len(head)] = np.frombuffer(head, np.uint8)
+    return rows, counts, overflow_from(counts, cap, lambda f: frame_records[f])
+
+
+def overflow_bytes(counts, cap: int) -> int:
+    """Size of the overflow message of a batch with these true per-frame counts."""
+    c = np.asarray(counts, np.int64)
+    return int(np.maximum(c - cap, 0).sum()) * _rec_size()
+
+
+def join_records(rows, counts, overflow, cap: int):
+    """Inverse of split_records: every frame's full at_detection bytes."""
+    rs = _rec_size()
+    rows = np.asarray(rows, np.uint8)
+    overflow = np.asarray(overflow, np.uint8)
+    out, pos = [], 0
+    for f, n in enumerate(np.asarray(counts, np.int64)):
+        n = int(n)
+        b = rows[f, :min(n, cap) * rs].tobytes()
+        if n > cap:
+            m = (n - cap) * rs
+            b += overflow[pos:pos + m].tobytes()
+            pos += m
+        out.append(b)
+    if pos != overflow.size:
+        raise ValueError("overflow holds %d bytes, the counts name %d" % (overflow.size, pos))
+    return out
+
+
+class RecordGather:
+    """Detection records of every rank's batch -> rank 0 (north-star topology), every
+    detection of every frame (the reference publishes all of them,
+    apriltags_cuda_detector.cu:420-465): one point-to-point message per peer and step
+    holds a fixed-capacity row per frame (its first `cap` records) and the frame's true
+    count; the records of frames with more than `cap` follow in a second message sized
+    by those counts.  RCCL with backend "nccl", gloo on CPU.  Double-buffered: the
+    transfer of step s overlaps the detection of the next steps.  Rank 0's own records
+    never move (they are already in its host buffer), so at world size 1 nothing is sent.
+
+    A peer's ``post(step, records, counts, overflow)``: `records` [batch, rec_bytes]
+    and `counts` [batch] int32 (host tensors; `records` page-locked, read by an async
+    copy -- the caller keeps it intact until ``copied`` of that step has completed),
+    `overflow` the bytes of split_records (None or empty: no frame above `cap`).
+    Rank 0's ``post(step)`` posts the receives; ``result(step)`` returns, per peer, the
+    [batch, 4 + rec_bytes] tensor (count, records) and the overflow bytes once arrived
+    (``frames(step)``: every frame's full record bytes).
+
+    Message order per peer (point-to-point order is the matching order): header(s),
+    overflow(s) if any, header(s + 1) ...  Rank 0 learns the size of overflow(s) from
+    header(s), so before posting header(s + 1) it waits for header(s) (one step behind
+    the detector) and posts the overflow receive first."""
 
     def __init__(self, dist, batch: int, rec_bytes: int, device):
         import torch
         self.dist, self.world, self.rank = dist, dist.get_world_size(), dist.get_rank()
+        self.device = device
         self.cuda = str(device).startswith("cuda")
+        self.batch, self.rec_bytes = batch, rec_bytes
+        self.cap = rec_bytes // _rec_size()
         row = rec_bytes + 4
         self.send = [torch.empty((batch, row), dtype=torch.uint8, device=device) for _ in range(2)]
         self.cnt = [torch.empty((batch,), dtype=torch.int32) for _ in range(2)]
@@ -173,40 +236,98 @@ class RecordGather:
             self.cnt = [c.pin_memory() for c in self.cnt]
         self.recv = ([{r: torch.empty((batch, row), dtype=torch.uint8, device=device) for r in range(1, self.world)}
                       for _ in range(2)] if self.rank == 0 else None)
-        self.work = [None, None]
-        self.copied = [None, None]  # event after step's copies out of the caller's host buffers
+        self.ovf = [None, None]      # peer: overflow send buffer; rank 0: {peer: receive buffer}
+        self.work = [None, None]     # header transfers of the slot
+        self.owork = [None, None]    # overflow transfers of the slot
+        self.unresolved = []         # rank 0: steps whose overflow receives are not posted yet
+        self.records_received = 0    # rank 0: records of the peers received (true counts)
+        self.copied = [None, None]   # event after step's copies out of the caller's host buffers
 
     def _wait(self, i):
+        for w in (self.work[i] or []) + (self.owork[i] or []):
+            w.wait()
+        self.work[i] = self.owork[i] = None
+
+    def _resolve(self, step):
+        """Rank 0: header(step) has to have arrived; post its overflow receives."""
+        import torch
+        i = step % 2
         for w in (self.work[i] or []):
             w.wait()
         self.work[i] = None
+        if self.cuda:
+            torch.cuda.current_stream().synchronize()  # the headers are in HBM: read their counts
+        ovf, ops = {}, []
+        for r in range(1, self.world):
+            counts = self.recv[i][r][:, :4].contiguous().view(torch.int32).ravel().cpu().numpy()
+            self.records_received += int(counts.sum())
+            m = overflow_bytes(counts, self.cap)
+            if m:
+                ovf[r] = torch.empty((m,), dtype=torch.uint8, device=self.device)
+                ops.append(self.dist.P2POp(self.dist.irecv, ovf[r], r))
+        self.ovf[i] = ovf
+        self.owork[i] = self.dist.batch_isend_irecv(ops) if ops else None
 
-    def post(self, step, records=None, counts=None):
+    def post(self, step, records=None, counts=None, overflow=None):
         import torch
         if self.world == 1:
             return
         d, i = self.dist, step % 2
-        self._wait(i)  # the buffer's previous transfer (step - 2)
         if self.rank == 0:
-            ops = [d.P2POp(d.irecv, self.recv[i][r], r) for r in range(1, self.world)]
-        else:
-            if self.copied[i] is not None:
-                self.copied[i].synchronize()  # (step - 2's copy of cnt[i]: long done)
-            self.cnt[i].copy_(counts)
-            self.send[i][:, 4:].copy_(records, non_blocking=True)
-            self.send[i][:, :4].copy_(self.cnt[i].view(torch.uint8).view(-1, 4), non_blocking=True)
-            if self.cuda:
-                self.copied[i] = torch.cuda.Event()
-                self.copied[i].record()
-            ops = [d.P2POp(d.isend, self.send[i], 0)]
-        self.work[i] = d.batch_isend_irecv(ops)
+            while self.unresolved:  # overflow(s) precedes header(s + 1) on every link
+                self._resolve(self.unresolved.pop(0))
+            self._wait(i)  # the buffer's previous transfer (step - 2)
+            self.work[i] = d.batch_isend_irecv([d.P2POp(d.irecv, self.recv[i][r], r) for r in range(1, self.world)])
+            self.unresolved.append(step)
+            return
+        self._wait(i)  # the buffer's previous transfer (step - 2)
+        if self.copied[i] is not None:
+            self.copied[i].synchronize()  # (step - 2's copy of cnt[i]: long done)
+        self.cnt[i].copy_(counts)
+        self.send[i][:, 4:].copy_(records, non_blocking=True)
+        self.send[i][:, :4].copy_(self.cnt[i].view(torch.uint8).view(-1, 4), non_blocking=True)
+        n_over = 0 if overflow is None else int(overflow.numel() if hasattr(overflow, "numel") else len(overflow))
+        if n_over != overflow_bytes(self.cnt[i].numpy(), self.cap):
+            raise ValueError("overflow of %d bytes does not match the counts" % n_over)
+        self.ovf[i] = None
+        if n_over:
+            o = overflow if hasattr(overflow, "numel") else torch.from_numpy(np.asarray(overflow, np.uint8))
+            self.ovf[i] = o.to(self.device, non_blocking=False) if self.cuda else o.clone()
+        if self.cuda:
+            self.copied[i] = torch.cuda.Event()
+            self.copied[i].record()
+        self.work[i] = d.batch_isend_irecv([d.P2POp(d.isend, self.send[i], 0)])
+        if n_over:
+            self.owork[i] = d.batch_isend_irecv([d.P2POp(d.isend, self.ovf[i], 0)])
 
     def result(self, step):
+        """Rank 0: {peer: (header [batch, 4 + rec_bytes], overflow bytes or None)}."""
         i = step % 2
-        self._wait(i)
-        return self.recv[i] if self.rank == 0 else None
+        if step in self.unresolved:
+            while self.unresolved and self.unresolved[0] <= step:
+                self._resolve(self.unresolved.pop(0))
+        for w in (self.owork[i] or []):
+            w.wait()
+        self.owork[i] = None
+        if self.rank != 0:
+            return None
+        return {r: (self.recv[i][r], self.ovf[i].get(r)) for r in range(1, self.world)}
+
+    def frames(self, step):
+        """Rank 0: {peer: [full at_detection bytes of each frame of its batch]}."""
+        import torch
+        out = {}
+        for r, (hdr, ovf) in self.result(step).items():
+            h = hdr.cpu()
+            counts = h[:, :4].contiguous().view(torch.int32).ravel().numpy()
+            o = ovf.cpu().numpy() if ovf is not None else np.zeros(0, np.uint8)
+            out[r] = join_records(h[:, 4:].numpy(), counts, o, self.cap)
+        return out
 
     def drain(self):
+        if self.rank == 0:
+            while self.unresolved:
+                self._resolve(self.unresolved.pop(0))
         self._wait(0)
         self._wait(1)
 

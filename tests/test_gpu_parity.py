@@ -362,7 +362,7 @@ def test_distortion_variants(gpu, oracle_mod, dist):
 
 
 @pytest.mark.parametrize("batch,timed", [(8, "k_blob"), (8, "k_boundary"), (1, "k_blob_small"), (8, "k_pose"),
-                                         (1, "k_decode")])
+                                         (1, "k_decode"), (8, "k_thr_ccl"), (192, "k_thr_ccl")])
 def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     """The bench's launch modes give identical detections: hipGraph replay, the
     split graph around a timed kernel (fence-free events between three graphs; on
@@ -370,7 +370,8 @@ def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     launches with events between every kernel).  The timer reports every launch."""
     import torch
     from ros_vision_amd import synth
-    frames = np.stack([synth.stream_frame(1280, 720, 20 + i)[0] for i in range(batch)])
+    distinct = np.stack([synth.stream_frame(1280, 720, 20 + i)[0] for i in range(min(batch, 8))])
+    frames = np.concatenate([distinct] * (-(-batch // distinct.shape[0])))[:batch]
     t = torch.from_numpy(frames).cuda()
     det = gpu.GpuDetector(1280, 720, max_batch=batch)
 
@@ -399,6 +400,34 @@ def test_timed_and_profiled_launches_match_graph(gpu, batch, timed):
     det.set_profiling(False)
     assert nb >= 2 and all(v > 0 for v in stages.values())
     assert run() == base
+
+
+def test_mixed_geometries_keep_the_merge_lds_limit(gpu, oracle_mod):
+    """k_ccl_merge's dynamic-LDS limit is a process-wide function attribute.
+    A 1920x1080 throughput detector (153,600 B of merge LDS per launch), then an 800x600
+    one created in the same process (78,400 B): the 1080p detector must still launch
+    and detect like the oracle."""
+    from ros_vision_amd import synth
+    big = gpu.GpuDetector(1920, 1080, max_batch=8)
+    small = gpu.GpuDetector(800, 600, max_batch=8)
+    f1080 = synth.stream_frame(1920, 1080, 5)[0]
+    res = big.detect_batch([f1080])
+    orc = oracle_mod.Oracle(1920, 1080)
+    orc.detect(f1080, 0)
+    assert len(res[0]) > 0 and compare_detections(res[0], orc.detections()) == []
+    g8, _ = synth.render_edge_board(800, 600, seed=1400, codes=dict(oracle_mod.family_entries()))
+    res = small.detect_batch([g8], gpu.AT_FMT_GRAY8)
+    orc = oracle_mod.Oracle(800, 600)
+    orc.detect(g8, 2)
+    assert compare_detections(res[0], orc.detections()) == []
+    res = big.detect_batch([f1080])
+    assert compare_detections(res[0], orc_1080(oracle_mod, f1080)) == []
+
+
+def orc_1080(oracle_mod, frame):
+    orc = oracle_mod.Oracle(1920, 1080)
+    orc.detect(frame, 0)
+    return orc.detections()
 
 
 def test_environment_cannot_truncate_the_pipeline(oracle_mod):

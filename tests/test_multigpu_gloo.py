@@ -41,13 +41,19 @@ def _worker(rank, world, port, W, H, nper, q):
         src = torch.from_numpy(frames)
     mine = multigpu.scatter_frames(dist, src, nper, (H, 2 * W), "cpu").numpy()
     o = ao.Oracle(W, H)
-    dets = []
+    recs = []
     for f in mine:
         o.detect(f, 0)
-        dets.append(o.detections())
-    packed = multigpu.pack_detections(dets, 16)
-    allp = multigpu.gather_detections(dist, packed, "cpu")
-    el, cnt = multigpu.reduce_max_sum(dist, 1.0 + rank, float(sum(len(d) for d in dets)), "cpu")
+        recs.append(multigpu.detection_records(o.detections()))
+    # the bench's record path: 2 records per frame in the fixed-size row, the rest overflow
+    rows, counts, over = multigpu.split_records(recs, 2)
+    g = multigpu.RecordGather(dist, nper, 2 * multigpu._rec_size(), "cpu")
+    g.post(0, torch.from_numpy(rows), torch.from_numpy(counts), over)
+    allp = None
+    if rank == 0:
+        allp = recs + [b for r in range(1, world) for b in g.frames(0)[r]]
+    g.drain()
+    el, cnt = multigpu.reduce_max_sum(dist, 1.0 + rank, float(counts.sum()), "cpu")
     if rank == 0:
         q.put((allp, el, cnt))
     dist.barrier()
@@ -68,16 +74,17 @@ def test_scatter_detect_gather_world2(oracle_mod):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert el == 2.0  # max over ranks
-    got = multigpu.unpack_detections(allp)
     codes = dict(oracle_mod.family_entries())
     o = oracle_mod.Oracle(W, H)
     total = 0
     for i in range(world * nper):
         o.detect(synth.to_yuyv(synth.render_board(W, H, seed=100 + i, ntags=4, codes=codes)[0]), 0)
         want = o.detections()
+        got = multigpu.records_to_dicts(allp[i])
         total += len(want)
-        assert [d["id"] for d in got[i]] == [d["id"] for d in want]
-        for a, b in zip(got[i], want):
+        assert len(want) > 2  # (every frame goes through the overflow message)
+        assert [d["id"] for d in got] == [d["id"] for d in want]
+        for a, b in zip(got, want):
             assert np.array_equal(a["p"], b["p"]) and np.array_equal(a["H"], b["H"])
     assert cnt == total
 
@@ -149,28 +156,35 @@ def _gather_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    B, rb = 3, 8
-    g = multigpu.RecordGather(dist, B, rb, "cpu")
+    B, cap = 3, 2
+    g = multigpu.RecordGather(dist, B, cap * multigpu._rec_size(), "cpu")
     got = []
-    for s in range(5):  # step s: rank r's record bytes = 10*r + s, counts = r + s + frame
-        recs = torch.full((B, rb), 10 * rank + s, dtype=torch.uint8)
-        cnt = torch.tensor([rank + s + f for f in range(B)], dtype=torch.int32)
-        g.post(s, recs, cnt)
+    for s in range(5):  # step s: frame f of rank r has r + s + f detections, ids 1000 r + 100 s + k
+        recs = [multigpu.detection_records(_fake_dets(rank, s, f)) for f in range(B)]
+        rows, counts, over = multigpu.split_records(recs, cap)
+        g.post(s, torch.from_numpy(rows), torch.from_numpy(counts), over)
         if s >= 1 and rank == 0:  # results of the previous step (double buffered)
-            res = g.result(s - 1)
-            got.append({r: (int(t[0, 4]), t[:, :4].contiguous().view(torch.int32).ravel().tolist()) for r, t in res.items()})
+            got.append({r: [[d["id"] for d in multigpu.records_to_dicts(b)] for b in fr]
+                        for r, fr in g.frames(s - 1).items()})
     if rank == 0:
-        res = g.result(4)
-        got.append({r: (int(t[0, 4]), t[:, :4].contiguous().view(torch.int32).ravel().tolist()) for r, t in res.items()})
+        got.append({r: [[d["id"] for d in multigpu.records_to_dicts(b)] for b in fr] for r, fr in g.frames(4).items()})
     g.drain()
-    q.put((rank, got))
+    q.put((rank, got, g.records_received))
     dist.barrier()
     dist.destroy_process_group()
 
 
+def _fake_dets(rank, step, frame):
+    n = rank + step + frame
+    return [dict(id=1000 * rank + 100 * step + k, hamming=k % 3, decision_margin=50.0 + k, H=np.eye(3) * k,
+                 c=np.array([k, 2.0 * k]), p=np.full((4, 2), 0.5 * k)) for k in range(n)]
+
+
 def test_record_gather_world3():
     """bench.py --ingest scatter: detection records of ranks 1..N-1 reach rank 0 by
-    point-to-point sends (rank 0's own never move), double-buffered over steps."""
+    point-to-point sends (rank 0's own never move), double-buffered over steps; frames
+    with more records than the fixed-size row holds send the rest in the overflow
+    message (0 .. 8 records per frame against a row of 2)."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -178,12 +192,87 @@ def test_record_gather_world3():
     procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
+    res = {r: (got, n) for r, got, n in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert len(res[0]) == 5
-    for s, step in enumerate(res[0]):
+    got, nrec = res[0]
+    assert len(got) == 5
+    for s, step in enumerate(got):
         assert sorted(step) == [1, 2]
         for r in (1, 2):
-            assert step[r] == (10 * r + s, [r + s + f for f in range(3)])
+            assert step[r] == [[d["id"] for d in _fake_dets(r, s, f)] for f in range(3)]
+    assert nrec == sum(r + s + f for r in (1, 2) for s in range(5) for f in range(3))
+
+
+def _dense_worker(rank, world, port, q):
+    """Rank 1 holds a batch of the oracle's detections of the 160-tag 1080p board (131
+    per frame) and of a 15-tag C2 frame, packed as bench.py packs them (rec_cap 32 in
+    the fixed-size row, overflow_from for the rest of the frame's records)."""
+    sys.path.insert(0, ROOT)
+    import json
+    import torch
+    import torch.distributed as dist
+    from ros_vision_amd import multigpu
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v = json.load(open(os.path.join(ROOT, "tests", "golden", "vectors.json")))
+    batch = [v["dense_1080p_160tags"]["detections"], v["c2_720p_f0"]["detections"],
+             v["dense_1080p_160tags"]["detections"], []]
+    B, rec_cap = len(batch), 32
+    g = multigpu.RecordGather(dist, B, rec_cap * multigpu._rec_size(), "cpu")
+    out = None
+    for s in range(3):
+        if rank == 0:
+            g.post(s)
+        else:
+            recs = [multigpu.detection_records(batch[(f + s) % B]) for f in range(B)]
+            counts = [len(r) // multigpu._rec_size() for r in recs]
+            rows = np.zeros((B, rec_cap * multigpu._rec_size()), np.uint8)
+            for f, r in enumerate(recs):
+                head = r[:rec_cap * multigpu._rec_size()]
+                rows[f, :len(head)] = np.frombuffer(head, np.uint8)
+            g.post(s, torch.from_numpy(rows), torch.tensor(counts, dtype=torch.int32),
+                   multigpu.overflow_from(counts, rec_cap, lambda f: recs[f]))
+    if rank == 0:
+        out = [[multigpu.records_to_dicts(b) for b in g.frames(s)[1]] for s in (1, 2)]
+    g.drain()
+    if rank == 0:
+        q.put((out, g.records_received))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_record_gather_keeps_dense_frames_world2():
+    """a peer frame with more detections than the fixed-size record
+    row (131 on the 160-tag 1080p golden board vs 32) reaches rank 0 whole, with every
+    field of every record (the reference publishes every detection,
+    apriltags_cuda_detector.cu:420-465)."""
+    import json
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out, nrec = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    v = json.load(open(os.path.join(ROOT, "tests", "golden", "vectors.json")))
+    batch = [v["dense_1080p_160tags"]["detections"], v["c2_720p_f0"]["detections"],
+             v["dense_1080p_160tags"]["detections"], []]
+    assert len(batch[0]) == 131
+    for k, s in enumerate((1, 2)):
+        for f in range(4):
+            want = batch[(f + s) % 4]
+            got = out[k][f]
+            assert len(got) == len(want)
+            for a, b in zip(got, want):
+                assert a["id"] == b["id"] and a["hamming"] == b["hamming"]
+                assert np.float32(a["decision_margin"]) == np.float32(b["decision_margin"])
+                for key in ("H", "c", "p"):
+                    assert np.array_equal(np.asarray(a[key]).ravel(), np.asarray(b[key], np.float64).ravel())
+    assert nrec == 3 * (2 * 131 + 15)

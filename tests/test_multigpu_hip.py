@@ -2,8 +2,9 @@
 
 Frames originate on rank 0 and are scattered (gloo, CPU), each rank moves its
 shard into HBM on torch's stream, hands that stream to its detector with
-at_stream_wait (no host synchronize), detects through the C ABI, and the
-fixed-capacity records are gathered to rank 0 and compared with the oracle.
+at_stream_wait (no host synchronize), detects through the C ABI, and every
+detection record is gathered to rank 0 (multigpu.RecordGather: fixed-size rows plus
+the overflow message) and compared with the oracle.
 The RCCL variant of the same flow is bench.py --ingest scatter.
 """
 import os
@@ -44,11 +45,18 @@ def _worker(rank, world, port, W, H, nper, q):
     det = GpuDetector(W, H, max_batch=nper)
     det.wait_stream(torch.cuda.current_stream().cuda_stream)
     det.enqueue_device(d_frames.data_ptr(), d_frames[0].numel(), nper)
-    dets = det.collect()
-    packed = multigpu.pack_detections(dets, 32)
-    allp = multigpu.gather_detections(dist, packed, "cpu")
+    counts = det.collect(counts_only=True)
+    # the bench's record path (rows of the first rec_cap records + the true counts, the
+    # rest of each frame in the overflow message); rec_cap 4 < 15 detections per frame
+    rec_cap = 4
+    rows, cnt, over = multigpu.split_records([det.frame_record_bytes(f) for f in range(nper)], rec_cap)
+    assert list(cnt) == counts
+    g = multigpu.RecordGather(dist, nper, rec_cap * multigpu._rec_size(), "cpu")
+    g.post(0, torch.from_numpy(rows), torch.from_numpy(cnt), over)
     if rank == 0:
+        allp = [det.frame_record_bytes(f) for f in range(nper)] + g.frames(0)[1]
         q.put(allp)
+    g.drain()
     dist.barrier()
     det.close()
     dist.destroy_process_group()
@@ -67,12 +75,12 @@ def test_hip_detector_in_process_group(oracle_mod):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    got = multigpu.unpack_detections(allp)
     o = oracle_mod.Oracle(W, H)
     for i in range(world * nper):
         o.detect(synth.stream_frame(W, H, 40 + i)[0], 0)
         want = o.detections()
+        got = multigpu.records_to_dicts(allp[i])
         assert len(want) == 15
-        assert [d["id"] for d in got[i]] == [d["id"] for d in want]
-        for a, b in zip(got[i], want):
+        assert [d["id"] for d in got] == [d["id"] for d in want]
+        for a, b in zip(got, want):
             assert np.allclose(a["p"], b["p"], atol=1e-4) and np.allclose(a["H"], b["H"], atol=1e-4)

@@ -412,3 +412,15 @@ def test_ros2_node_type_checks():
                         "-I" + NODE, os.path.join(NODE, "ros2_apriltags_node.cpp")],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_mock_node_rejects_timing_without_frames(built, tmp_path):
+    """`--time` over zero frames (--count 0 or an empty frames file) exits 2
+    with a message before the timed loop (its `% count` would divide by zero)."""
+    empty = tmp_path / "empty.bgr"
+    empty.write_bytes(b"")
+    for extra in ([], ["--count", "0"]):
+        r = subprocess.run([os.path.join(built, "at_mock_node"), "--width", "64", "--height", "64", "--format",
+                            "gray", "--frames", str(empty), "--time", "5"] + extra,
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2 and "--time needs at least one frame" in r.stderr, (r.returncode, r.stderr)

@@ -1,9 +1,10 @@
 """GPU parity of the exact configurations the bench reports.
 
 * C2 headline: bench.py's own loop (ros_vision_amd.stream.StreamRunner) with
-  its defaults -- 4 detector instances x max_batch 128, enqueue_device / collect
-  round-robin over the 64-frame C2 pool replicated 4x in HBM, hipGraph replay,
-  then again with the live kernel timer (the split graphs of the timed region).
+  its defaults imported from bench.py (instances, batch, HBM pool copies,
+  DOMINANT) -- enqueue_device / collect round-robin over the 64-frame C2 pool in
+  HBM, hipGraph replay, then again with the live kernel timer on the dominant
+  kernel (the split graphs of the timed region).
   Every frame of every batch is compared with the committed oracle goldens.
 * C4 geometry in throughput mode: 8 1920x1080 frames, max_batch 8 (the
   throughput-mode kernels), stage-by-stage against the live oracle and against
@@ -30,12 +31,22 @@ def c2():
 
 
 def test_bench_headline_configuration(c2):
+    """bench.py's headline configuration exactly: its defaults (instances, batch, the HBM
+    pool copies, the kernel timer on DOMINANT) are imported from bench.py, so a changed
+    bench default changes what this test runs.  8 batches with graph replay, then 8
+    under the live kernel timer (the launch sequence as three graphs cut around the
+    timed kernel -- the bench's timed region); every frame of every batch against the
+    oracle goldens."""
     import torch
 
+    import bench
+    import make_stream_golden as mg
     import ros_vision_amd as rva
     from ros_vision_amd.stream import StreamRunner
     g, frames = c2
-    instances, B, copies = 4, 128, 4  # bench.py defaults
+    args = bench.parse([])
+    instances, B, copies, timed = args.instances, args.batch, bench.pool_copies(args), bench.DOMINANT
+    assert (args.width, args.height, args.tags, args.pool) == (1280, 720, 15, frames.shape[0])
     pool = frames.shape[0]
     d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
     stride = frames[0].nbytes
@@ -58,17 +69,18 @@ def test_bench_headline_configuration(c2):
     assert seen["frames"] == 8 * B and n == seen["dets"] == 8 * B * 15
     # the timed region of the bench: the kernel timer splits the graph around its kernel
     for d in dets:
-        d.set_kernel_timer("k_blob_small")
-    runner.run(4, 8, on_batch=check)
+        d.set_kernel_timer(timed)
+    n = runner.run(8, 8, on_batch=check)
     assert bad == [], bad[:10]
-    ms = [d.kernel_time() for d in dets]
-    assert all(k > 0 and launches == 1 for k, launches in ms)
+    assert seen["frames"] == 16 * B and n == 8 * B * 15
+    per = 8 // instances
+    assert all(ms > 0 and launches == per for ms, launches in (d.kernel_time() for d in dets))
+    assert all(ms > 0 and launches == per for ms, launches in (d.kernel_span() for d in dets))
     for d in dets:
         d.set_kernel_timer(None)
     # intermediate planes of each instance's last batch: threshold + labels bit-exact
-    import make_stream_golden as mg
     for d in dets[:2]:
-        off = runner.offset(8 + dets.index(d))
+        off = runner.offset(12 + dets.index(d))
         for j in (0, 1, B - 1):
             f = (off + j) % pool
             assert mg.digest(d.copy_thresholded(j)) == g["thr_digest"][f]
