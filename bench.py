@@ -93,7 +93,16 @@ def parse(argv=None):
                     help="local: every rank renders its own frames into its HBM (weak scaling, no data-path "
                          "collective); scatter: frames live on rank 0 and are scattered each step over RCCL "
                          "(north-star topology), detection records gathered back to rank 0")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def pool_copies(args):
+    """Copies of the --pool frames resident per GPU: at least 4 and two batches' worth,
+    so consecutive steps read different frames, all from HBM (rank 0's scatter pool per
+    rank follows the same rule)."""
+    if args.hbm_copies:
+        return max(1, args.hbm_copies)
+    return max(4, -(-2 * args.batch // args.pool))
 
 
 def kernel_algorithmic_bytes(kernel, stats, W, H):
@@ -538,10 +547,12 @@ def main():
         kk = [v for k, v in (pmc or {}).get("kernels", {}).items() if k.split("<")[0] == kernel]
         return round(B * sum(2 * v["fetch_bytes_per_frame"] + v["write_bytes_per_frame"] for v in kk)) if kk else None
 
-    # headline roofline: the kernel with the longest isolated launch (one batch in
-    # flight), its device-clock span in this run
+    # headline roofline: the DOMINANT kernel (fixed rule: the largest marginal cost in
+    # the concurrent loop) with its launch measured in isolation (one batch in flight),
+    # its device-clock span in this run; the longest isolated kernel is named beside it
     iso_rows = isolated_table(iso, W, H)
-    head = iso_rows[0] if iso_rows else None
+    head = next((r for r in iso_rows if r["kernel"] == dominant), None)
+    longest = iso_rows[0]["kernel"] if iso_rows else None
     # concurrent: the DOMINANT kernel timed inside the timed region (four batches in flight)
     kbytes = kernel_algorithmic_bytes(dominant, stats, W, H)
     k_achieved = kbytes / (k_ms * 1e-3) / 1e9 if (kbytes and k_ms > 0) else None
@@ -553,15 +564,18 @@ def main():
                     "algorithmic_bytes_per_launch": head["algorithmic_bytes_per_launch"],
                     "avg_launch_ms": head["avg_launch_ms_device_clock"],
                     "avg_launch_ms_hip_events": head["avg_launch_ms_hip_events"], "launches_timed": head["launches"],
+                    "longest_isolated_kernel": longest, "differs_from_longest_isolated": longest != head["kernel"],
                     "isolated": iso_rows,
-                    "note": "the launch sequence's longest kernel, measured in isolation in this run: one batch of "
+                    "note": "DOMINANT (fixed rule: the largest marginal cost in the concurrent loop, "
+                            "profiles/r04c/ablation.txt) measured in isolation in this run: one batch of "
                             "%d frames in flight (enqueue, collect), the kernel timer on one kernel at a time, "
                             "avg_launch_ms = its execution span on the device wall clock (first workgroup start "
                             "to last workgroup end, at_kernel_span: what a rocprofv3 kernel trace reports; "
                             "`bench.py --isolated-only` under rocprofv3 --kernel-trace reproduces it, "
                             "profiles/); algorithmic bytes per DESIGN.md section 4; traffic = PMC "
                             "(2*FETCH_SIZE+WRITE_SIZE) per launch from profiles/pmc_traffic.json; `isolated`: "
-                            "every kernel the same way" % B}
+                            "every kernel the same way, longest first (the top three are within ~10 %% of each "
+                            "other and change places between boxes)" % B}
     else:
         roofline = None
     roofline_concurrent = {

@@ -162,6 +162,57 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 // and the last end -- the kernel's execution span, as rocprofv3's kernel trace
 // times it, measured live without a profiler.  Nothing is stored unless this
 // launch is the timed one.
+// XCD-aware tile order.  Workgroups are dealt round-robin over the chip's 8 XCDs
+// (MI355X_MICROARCH.md, Workgroup dispatch: blocks b and b + 8 share one), each with
+// its own L2.  In blockIdx order, horizontally adjacent tiles -- which share the
+// 64-B sectors of their halo columns and, for 64-pixel-wide decimated tiles, the
+// 128-B lines of every row -- land on different XCDs and each fetches the shared
+// sectors from the fabric.  xcd_block() renumbers the grid so that XCD k (the blocks
+// b = k mod 8, in dispatch order) takes the k-th contiguous range of the (z, y, x)
+// tile order: neighbours share an XCD and its L2.  A bijection for any grid size
+// (XCDs 0 .. n%8-1 take one block more); placement-independent for correctness.
+// Modes: 0 = blockIdx order; 1 = XCD k takes the k-th contiguous eighth of the
+// (z, y, x) order; 2 = row chunks: XCD k takes grid rows (y, z) = k, k + 8, k + 16 ...
+// whole (horizontal neighbours share the XCD, the 8 XCDs stay on nearby rows).
+#ifndef AT_XCD_PRE
+#define AT_XCD_PRE 1
+#endif
+#ifndef AT_XCD_THR
+#define AT_XCD_THR 1
+#endif
+#ifndef AT_XCD_BND
+#define AT_XCD_BND 0
+#endif
+#ifndef AT_XCD_GRP
+#define AT_XCD_GRP 0
+#endif
+struct TileIdx {
+  int x, y, z;
+};
+template <int MODE>
+__device__ __forceinline__ TileIdx xcd_block() {
+  if constexpr (MODE == 0) return TileIdx{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const uint32_t gx = gridDim.x, gxy = gridDim.x * gridDim.y, n = gxy * gridDim.z;
+  const uint32_t lid = blockIdx.x + gx * blockIdx.y + gxy * blockIdx.z;
+  uint32_t t;
+  if constexpr (MODE == 1) {
+    const uint32_t q = n >> 3, r = n & 7, xcd = lid & 7;
+    t = xcd * q + min(xcd, r) + (lid >> 3);
+  } else {
+    // rows in complete groups of 8 (the first n8 blocks: the same count on every
+    // XCD), the last partial group in blockIdx order
+    const uint32_t rows = n / gx, n8 = (rows & ~7u) * gx;
+    if (lid < n8) {
+      const uint32_t k = lid >> 3, j = k / gx;
+      t = ((j << 3) + (lid & 7)) * gx + (k - j * gx);
+    } else {
+      t = lid;
+    }
+  }
+  const uint32_t z = t / gxy, rem = t - z * gxy, y = rem / gx;
+  return TileIdx{(int)(rem - y * gx), (int)y, (int)z};
+}
+
 __device__ __forceinline__ uint32_t kt_wg_id() {
   return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
 }
@@ -248,9 +299,10 @@ __device__ __forceinline__ void load_y8(const uint8_t* in, int W, int row, int x
 // already, so k_decode samples the frame and the plane is not written
 template <int FMT>
 __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g, int wgray) {
-  const int f = blockIdx.z;
-  const int tx = blockIdx.x * 64 + threadIdx.x;
-  const int ty = blockIdx.y * 4 + threadIdx.y;
+  const TileIdx bi = xcd_block<AT_XCD_PRE>();
+  const int f = bi.z;
+  const int tx = bi.x * 64 + threadIdx.x;
+  const int ty = bi.y * 4 + threadIdx.y;
   // the batch's control block starts at zero (no memset node): nothing in k_pre
   // reads it, every later kernel follows in stream order
   if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
@@ -376,9 +428,10 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES;
   constexpr int kTW = kCclTileW / 4, kTH = kCclTileH / 4;  // 4x4 threshold tiles per CCL tile
   constexpr int kHR = kCclTileH + 1, kHC = kCclTileW + 2;  // threshold halo: rows y0-1.., cols x0-1..x0+W
-  const int f = blockIdx.z;
+  const TileIdx bi = xcd_block<AT_XCD_THR>();
+  const int f = bi.z;
   const int tid = threadIdx.x;
-  const int y0 = blockIdx.y * kCclTileH, x0 = blockIdx.x * kCclTileW;
+  const int y0 = bi.y * kCclTileH, x0 = bi.x * kCclTileW;
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
   const uint8_t* mm = b.mm + (size_t)f * g.TW * g.TH * 2;
   uint8_t* thr = b.thr + (size_t)f * g.Wd * g.Hd;
@@ -733,7 +786,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
     if (lR) s_li[R] = (uint16_t)iR;
     __syncthreads();  // (the descriptor below reads other threads' roots' slots)
   }
-  const size_t tl = (size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x;
+  const size_t tl = (size_t)f * g.CTX * g.CTY + bi.y * g.CTX + bi.x;
   if (inimg) {
     auto gid = [&](uint32_t s) -> uint32_t { return s_gid[s]; };
     uint32_t* par = b.par + (size_t)f * g.Wd * g.Hd;
@@ -811,7 +864,7 @@ __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT
   __syncthreads();
   ph(9);
   if (tid == 0) {
-    b.nlroot[(size_t)f * g.CTX * g.CTY + blockIdx.y * g.CTX + blockIdx.x] = s_nlr;
+    b.nlroot[(size_t)f * g.CTX * g.CTY + bi.y * g.CTX + bi.x] = s_nlr;
     kt_end(b, 1);
   }
 }
@@ -1374,7 +1427,8 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   // only when both blobs are kept; the dedup rule's "!= 127 and kept" likewise)
   __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
   __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
-  const int f = blockIdx.z;
+  const TileIdx bi = xcd_block<AT_XCD_BND>();
+  const int f = bi.z;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   kt_begin(b, 4);
   for (int i = tid; i < kLdsPairSlots; i += 256) {
@@ -1389,7 +1443,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   const uint8_t* thr = b.thr + fo;
   const uint32_t* par = b.par + fo;
   const int Wd = g.Wd;
-  const int ty0 = 1 + blockIdx.y * (4 * kBndRows), tx0 = blockIdx.x * 64;  // halo origin: x0 - 1
+  const int ty0 = 1 + bi.y * (4 * kBndRows), tx0 = bi.x * 64;  // halo origin: x0 - 1
   constexpr int kTR = 4 * kBndRows + 1, kTC = 66, kTN = kTR * kTC;
   constexpr int kPer = (kTN + 255) / 256;
   // label of a pixel = par[par[node]]: its block node (fg -> F, bg -> L / R by
@@ -1429,9 +1483,9 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     }
   }
   __syncthreads();  // LDS tables initialised
-  const int x = 1 + blockIdx.x * 64 + threadIdx.x;
+  const int x = 1 + bi.x * 64 + threadIdx.x;
   const uint32_t lane = lane_id();
-  const size_t tb = (size_t)f * g.ntb + blockIdx.y * gridDim.x + blockIdx.x;
+  const size_t tb = (size_t)f * g.ntb + bi.y * gridDim.x + bi.x;
   uint64_t* pts_out = b.pts + tb * g.bnd_region;
   for (int r = 0; r < kBndRows; r++) {
     const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
@@ -1946,12 +2000,13 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 constexpr int kGrpPre = 2;
 constexpr int kGrpEntPre = 32;
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
-  const int f = blockIdx.y;
+  const TileIdx bi = xcd_block<AT_XCD_GRP>();
+  const int f = bi.y;
   __shared__ uint64_t s_hk[2 * kGrpEnt];
   __shared__ uint32_t s_he[2 * kGrpEnt];
   __shared__ uint32_t s_base[kGrpEnt], s_cur[kGrpEnt];
   const int tid = threadIdx.x;
-  const size_t tb = (size_t)f * g.ntb + blockIdx.x;
+  const size_t tb = (size_t)f * g.ntb + bi.x;
   const uint64_t* pts = b.pts + tb * g.bnd_region;
   // one round trip: status, counters, entry, points (the first 512 8-B keys or
   // 1024 narrow words: the same bytes)

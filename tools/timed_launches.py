@@ -16,7 +16,7 @@ import sys
 
 def main(trace_csv, bench_json):
     line = json.load(open(bench_json))
-    rf = line["roofline"]
+    rf = line.get("roofline_concurrent") or line["roofline"]  # (the timed loop's live timer)
     kern, k = rf["kernel"], line["steps"]
     rows = [r for r in csv.DictReader(open(trace_csv)) if r["Kernel_Name"].split("(")[0].split("<")[0].endswith(kern)]
     # the bench's batch size is in its grid (k_* kernels of other batch sizes are
