@@ -749,6 +749,7 @@ static int collect(at_detector* d, at_detection* out, int cap_per_frame, int* n_
     d->kt_n++;
     uint64_t st[2];
     memcpy(st, d->h_ctrl + d->kstamp_word, sizeof(st));
+    st[0] = ~st[0];  // (k_kt_span keeps the complement of the first start: atomicMax on a zeroed word)
     if (st[1] > st[0] && st[0] && d->wclk_khz > 0) {  // (kernels without stamps leave zeros)
       d->kd_ms += (double)(st[1] - st[0]) / d->wclk_khz;
       d->kd_n++;

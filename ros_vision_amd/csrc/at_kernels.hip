@@ -189,6 +189,19 @@ __device__ T block_incl_scan(T v, T* s_tmp, T* total, int NW) {
 struct TileIdx {
   int x, y, z;
 };
+// a / d for a, d < 2^24 (grid sizes): a float reciprocal and two correction steps
+// instead of the ~40-instruction integer division (k_boundary: +2.7 % with it)
+__device__ __forceinline__ uint32_t udiv24(uint32_t a, uint32_t d) {
+  // (v_rcp_f32 within 1 ulp, the product rounded: q is off by at most 2)
+  uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)d));
+  int32_t r = (int32_t)(a - q * d);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (r < 0) { q--; r += (int32_t)d; }
+    if (r >= (int32_t)d) { q++; r -= (int32_t)d; }
+  }
+  return q;
+}
 template <int MODE>
 __device__ __forceinline__ TileIdx xcd_block() {
   if constexpr (MODE == 0) return TileIdx{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
@@ -201,15 +214,15 @@ __device__ __forceinline__ TileIdx xcd_block() {
   } else {
     // rows in complete groups of 8 (the first n8 blocks: the same count on every
     // XCD), the last partial group in blockIdx order
-    const uint32_t rows = n / gx, n8 = (rows & ~7u) * gx;
+    const uint32_t rows = gridDim.y * gridDim.z, n8 = (rows & ~7u) * gx;
     if (lid < n8) {
-      const uint32_t k = lid >> 3, j = k / gx;
+      const uint32_t k = lid >> 3, j = udiv24(k, gx);
       t = ((j << 3) + (lid & 7)) * gx + (k - j * gx);
     } else {
       t = lid;
     }
   }
-  const uint32_t z = t / gxy, rem = t - z * gxy, y = rem / gx;
+  const uint32_t z = udiv24(t, gxy), rem = t - z * gxy, y = udiv24(rem, gx);
   return TileIdx{(int)(rem - y * gx), (int)y, (int)z};
 }
 
@@ -227,24 +240,23 @@ __device__ __forceinline__ void kt_end(const DevBufs& b, int stage) {  // one th
   const uint32_t id = kt_wg_id();
   if (id < b.kwg_cap) b.kwg[b.kwg_cap + id] = wall_clock64();
 }
+// kKtSpanWgs workgroups, each a strided share of the stamps, combined by 64-bit
+// atomicMax into the control block (zeroed at the batch start): [0] holds the
+// complement of the first start, [1] the last end.  One workgroup walking all
+// 23,040 stamps of a 192-frame k_thr_ccl launch took 43 us on the batch's chain.
+constexpr int kKtSpanWgs = 32;
 __global__ __launch_bounds__(256) void k_kt_span(DevBufs b) {
-  __shared__ uint64_t s_mn[4], s_mx[4];
   const uint32_t n = min(*b.kgrid, b.kwg_cap);
   uint64_t mn = ~0ull, mx = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += 256) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += kKtSpanWgs * 256) {
     mn = min(mn, b.kwg[i]);
     mx = max(mx, b.kwg[b.kwg_cap + i]);
   }
   mn = wave_reduce(mn, MinOp());
   mx = wave_reduce(mx, MaxOp());
-  if (lane_id() == 0) { s_mn[threadIdx.x >> 6] = mn; s_mx[threadIdx.x >> 6] = mx; }
-  __syncthreads();
-  if (threadIdx.x == 0 && n) {
-    for (int w = 1; w < 4; w++) { mn = min(mn, s_mn[w]); mx = max(mx, s_mx[w]); }
-    mn = min(mn, s_mn[0]);
-    mx = max(mx, s_mx[0]);
-    b.kstamp[0] = mn;
-    b.kstamp[1] = mx;
+  if (lane_id() == 0 && mx) {
+    atomicMax((unsigned long long*)&b.kstamp[0], (unsigned long long)~mn);
+    atomicMax((unsigned long long*)&b.kstamp[1], (unsigned long long)mx);
   }
 }
 
@@ -5065,7 +5077,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   // the timed kernel's device-clock span (after it, outside its timing events;
   // before k_pose hands the control block to the host)
   if (b.kt_stage >= 1 && b.kt_stage <= 10 && b.kt_stage != 3 && b.kt_stage != 5 && b.kt_stage != 6)
-    hipLaunchKernelGGL(k_kt_span, dim3(1), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(k_kt_span, dim3(kKtSpanWgs), dim3(256), 0, st, b);
   tk(11, st, 0);
   // latency mode: a wave per detection; throughput mode: four lanes per detection
   if (prm.tag_size > 0 && on(11) && !pose_fused) {

@@ -19,6 +19,13 @@ fi
 if [ -n "${BENCH:-}" ]; then
   timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 fi
+if [ -n "${TIMER_AB:-}" ]; then  # the timed region with and without the live kernel timer, interleaved
+  LEG="--no-cpu-baseline --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --no-stage-profile --isolated-batches 0"
+  for r in 1 2 3; do for t in "" "--no-kernel-timer"; do
+    echo -n "round=$r timer=${t:-on} " >> $O/timer_ab.txt
+    timeout -k 10 200 python3 bench.py $LEG $t 2>>$O/timer_ab.err | python3 -c "import json,sys; j=json.load(sys.stdin); print(j['value'], j['ms_per_step'])" >> $O/timer_ab.txt || exit 1
+  done; done
+fi
 if [ -n "${LIBS:-}" ]; then TAG=$TAG bash tools/ab_stages.sh > /dev/null || exit 1; fi
 if [ -n "${PMCLIBS:-}" ]; then LIBS="$PMCLIBS" TAG=$TAG/pmc bash tools/pmc_ab.sh > $O/pmc_ab.txt 2> $O/pmc_ab.err || exit 1; fi
 if [ -n "${ISO:-}" ]; then
