@@ -9,7 +9,7 @@
  *
  * libm transcendental calls of the reference (atan2f, cosf, sinf, hypotf) are
  * replaced by the deterministic functions det_* below (double-precision
- * Cephes-style evaluations rounded to float).  They are within 1 float ulp of
+ * evaluations -- fdlibm / Cephes polynomials -- rounded to float).  They are within 1 float ulp of
  * libm; the HIP path evaluates the identical operation sequence.
  */
 #include "ao_oracle.h"
@@ -22,49 +22,43 @@
 /* ------------------------------------------------------------------------- */
 /* deterministic math                                                          */
 /* ------------------------------------------------------------------------- */
-static const double kAtanP[5] = {-8.750608600031904122785E-1, -1.615753718733365076637E1,
-                                 -7.500855792314704667340E1, -1.228866684490136173410E2,
-                                 -6.485021904942025371773E1};
-static const double kAtanQ[5] = {2.485846490142306297962E1, 1.650270098316988542046E2,
-                                 4.328810604912902668951E2, 4.853903996359136964868E2,
-                                 1.945506571482613964425E2};
-static const double kMoreBits = 6.123233995736765886130E-17;
 static const double kPi = 3.14159265358979323846;
 static const double kPio2 = 1.57079632679489661923;
-static const double kPio4 = 0.78539816339744830962;
 
-static double det_atan_pos(double t) {
-  double y0, x;
-  int flag;
-  if (t > 2.41421356237309504880) {
-    y0 = kPio2; flag = 1; x = -1.0 / t;
-  } else if (t <= 0.66) {
-    y0 = 0.0; flag = 0; x = t;
-  } else {
-    y0 = kPio4; flag = 2; x = (t - 1.0) / (t + 1.0);
-  }
-  double z = x * x;
-  double p = kAtanP[0];
-  for (int i = 1; i < 5; i++) p = p * z + kAtanP[i];
-  double q = z + kAtanQ[0];
-  for (int i = 1; i < 5; i++) q = q * z + kAtanQ[i];
-  z = z * p / q;
-  z = x * z + x;
-  if (flag == 2) z = z + 0.5 * kMoreBits;
-  else if (flag == 1) z = z + kMoreBits;
-  return y0 + z;
-}
-
+/* atan2 with one division (ros_vision_amd/csrc/at_detmath.h det_atan2, the same
+ * operation sequence): octant reduction t = (b - a) / (a + b) or b / a, |t| <= tan(pi/8),
+ * fdlibm's odd minimax polynomial for atan on |t| < 7/16 (s_atan.c) by explicit fma
+ * (correctly rounded), the octant constants in two parts. */
+static const double kAtanT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                                  1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                                  9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                  6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                                  4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                                  1.62858201153657823623e-02};
 static double det_atan2(double y, double x) {
-  if (x == 0.0) {
-    if (y > 0.0) return kPio2;
-    if (y < 0.0) return -kPio2;
-    return 0.0;
-  }
-  double a = det_atan_pos(fabs(y) / fabs(x));
-  if (x < 0.0) a = kPi - a;
-  if (y < 0.0) a = -a;
-  return a;
+  const double ax = fabs(x), ay = fabs(y);
+  const int sw = ay > ax;
+  const double a = sw ? ay : ax, b = sw ? ax : ay;
+  if (a == 0.0) return 0.0;
+  const int s = b > 0.41421356237309504880 * a;
+  const double t = (s ? b - a : b) / (s ? a + b : a);
+  const double z = t * t, w = z * z;
+  double s1 = fma(w, kAtanT[10], kAtanT[8]);
+  s1 = fma(w, s1, kAtanT[6]);
+  s1 = fma(w, s1, kAtanT[4]);
+  s1 = fma(w, s1, kAtanT[2]);
+  s1 = fma(w, s1, kAtanT[0]);
+  s1 = z * s1;
+  double s2 = fma(w, kAtanT[9], kAtanT[7]);
+  s2 = fma(w, s2, kAtanT[5]);
+  s2 = fma(w, s2, kAtanT[3]);
+  s2 = fma(w, s2, kAtanT[1]);
+  s2 = w * s2;
+  const double hi = s ? 7.85398163397448278999e-01 : 0.0, lo = s ? 3.06161699786838301793e-17 : 0.0;
+  double r = hi - ((t * (s1 + s2) - lo) - t);
+  if (sw) r = (1.57079632679489655800e+00 - r) + 6.12323399573676603587e-17;
+  if (x < 0.0) r = (3.14159265358979311600e+00 - r) + 1.22464679914735317723e-16;
+  return y < 0.0 ? -r : r;
 }
 
 /* Sensitivity hook (tools/fp_sensitivity.py, tests only): bit k of ao_fp_perturb
