@@ -34,6 +34,9 @@ namespace at {
 // small device helpers
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+// det_atan2f as a call: k_decode's refine evaluates it four times per quad, and its
+// polynomial constants inlined there cost spills (VGPR spills 16 -> 27)
+__device__ __attribute__((noinline)) float det_atan2f_call(float y, float x) { return det_atan2f(y, x); }
 
 __device__ __forceinline__ uint64_t mix_hash(uint64_t k) {
   return (k * 0x9E3779B97F4A7C15ull) >> (64 - kHashBits);
@@ -433,68 +436,16 @@ constexpr uint32_t kTouchBit = 0x80000000u;
 // planes written for the later stages), plus the decimated samples of the
 // 8-pixel halo its filtered tile min/max needs, so there is no min/max plane,
 // no re-read of the decimated plane and one launch less.
-#ifndef AT_THR_PIPE
-#define AT_THR_PIPE 0
-#endif
-// k_thr_ccl_pipe (PIPE): the tile's decimated samples with the 8-pixel halo the filtered
-// min/max needs, rows y0-8 .. y0+35 x dwords (x0/4)-2 .. (x0/4)+17, land in this LDS
-// staging area by LDS-DMA (global_load_lds_dword: no VGPRs held), issued while the
-// previous tile is labeled.  A file-scope array: the compiler sees it apart from the
-// tile's other LDS arrays, so their accesses do not wait for the DMA in flight.
-constexpr int kStageRows = kCclTileH + 12, kStageDw = 20, kStageChunks = (kStageRows * kStageDw + 63) / 64;
-__shared__ __attribute__((aligned(16))) uint32_t s_thr_stage[kStageChunks * 64];
-
-// the next tile's staging loads: 14 wave-instructions of 64 dwords over the 8 waves;
-// rows / dwords outside the frame read clamped addresses (masked by the users)
-__device__ __forceinline__ void thr_stage_issue(const DevBufs& b, const Geom& g, TileIdx nb) {
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const uint8_t* ndec = b.dec + (size_t)nb.z * g.Wd * g.Hd;
-  const int ny0 = nb.y * kCclTileH, ndw = nb.x * 16 - 2, wd4 = g.Wd >> 2;
-  for (int ch = w; ch < kStageChunks; ch += 8) {
-    const int d = ch * 64 + lane, r = d / kStageDw, c = d - r * kStageDw;
-    const int yc = min(max(ny0 - 8 + r, 0), g.Hd - 1), xc = min(max(ndw + c, 0), wd4 - 1);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(ndec + (size_t)yc * g.Wd) + xc;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(s_thr_stage + ch * 64));  // (wave-uniform)
-    // (inline asm, not the builtin: the compiler's wait insertion would otherwise guard
-    // later LDS stores it cannot tell apart from the DMA target with vmcnt(0), which waits
-    // for the prefetch; the loop head's explicit vmcnt(0) + barrier publishes the data)
-    // (M0 -- the LDS base of the DMA -- is a register the compiler reserves: saved and restored here)
-    uint32_t m0_saved;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_nop 0\n\ts_mov_b32 m0, %0"
-                 : "=&s"(m0_saved)
-                 : "v"(src), "s"(dst)
-                 : "memory");
-  }
-}
-
-// workgroup barrier for LDS only: this wave's LDS operations complete, then s_barrier;
-// no vmcnt wait (the staging DMA of the next tile stays in flight) and a compiler
-// memory barrier (no LDS access moves across it)
-template <bool PIPE>
-__device__ __forceinline__ void thr_sync() {
-  if constexpr (PIPE) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else __syncthreads();
-}
-
-// One CCL tile.  k_thr_ccl: one workgroup per tile (bi from the XCD-aware order);
-// k_thr_ccl_pipe (PIPE): a persistent workgroup's current tile, its samples in
-// s_thr_stage; once they are read, the next tile's staging DMA is issued (nb, if has_next).
-template <int TWD, int PRE, bool PIPE>
-__device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, const Params& prm, const TileIdx bi,
-                                             bool has_next, TileIdx nb) {
+// One CCL tile (k_thr_ccl: one workgroup per tile, bi from the XCD-aware order).
+template <int TWD, int PRE>
+__device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, const Params& prm, const TileIdx bi) {
   using CT = CclTile<TWD>;
   constexpr int NT = CT::NT;
   constexpr int kCclTileW = CT::W, kCclBW = CT::BW, kCclTileNodes = CT::NODES;
   constexpr int kTW = kCclTileW / 4, kTH = kCclTileH / 4;  // 4x4 threshold tiles per CCL tile
   constexpr int kHR = kCclTileH + 1, kHC = kCclTileW + 2;  // threshold halo: rows y0-1.., cols x0-1..x0+W
-  static_assert(!PIPE || (TWD == 64 && PRE < 0), "pipelined tiles: throughput mode");
   const int f = bi.z;
-  int tid_ = threadIdx.x;
-  // (pipelined: an opaque copy per tile, so the compiler recomputes what derives from
-  // the thread index inside the tile loop instead of holding it in VGPRs across tiles)
-  if constexpr (PIPE) asm volatile("" : "+v"(tid_));
-  const int tid = tid_;
+  const int tid = threadIdx.x;
   const int y0 = bi.y * kCclTileH, x0 = bi.x * kCclTileW;
   const uint8_t* dec = b.dec + (size_t)f * g.Wd * g.Hd;
   const uint8_t* mm = b.mm + (size_t)f * g.TW * g.TH * 2;
@@ -527,10 +478,10 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     // reads it, every later kernel follows in stream order
     if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
       for (uint32_t w = tid; w < b.ctrl_words; w += NT) b.ctrl[w] = 0;
-      thr_sync<PIPE>();
+      __syncthreads();
     }
   }
-  if constexpr (!PIPE) kt_begin(b, 1);
+  kt_begin(b, 1);
   // AT_PHASE_PROBE (throughput mode): per-phase wall-clock of workgroup thread 0
   // summed over the launch in probe[48 + k], workgroups in probe[63]
   uint64_t t_ph = 0;
@@ -542,39 +493,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     t_ph = t;
   };
   ph(0);
-  if constexpr (PIPE) {
-    // the staged samples (s_thr_stage, landed: the caller waited): unfiltered min/max of
-    // the staged 4x4 tiles (staging dword c of rows 4r .. 4r+3 is tile (r, c)), and the
-    // threshold windows (window j of halo row r: bytes 7+4j .. 10+4j of staging row r+7)
-    (void)dv;
-    for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
-      const int r = i / (kTW + 4), c = i % (kTW + 4);
-      const int tr = ty0 - 2 + r, tc = tx0 - 2 + c;
-      uint32_t mn = 255, mx = 0;  // out of range: neutral for min/max
-      if (tr >= 0 && tr < g.TH && tc >= 0 && tc < g.TW) {
-#pragma unroll
-        for (int dr = 0; dr < 4; dr++) {
-          const uint32_t w = s_thr_stage[(4 * r + dr) * kStageDw + c];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            mn = min(mn, (w >> (8 * k)) & 0xff);
-            mx = max(mx, (w >> (8 * k)) & 0xff);
-          }
-        }
-      }
-      s_umn[r][c] = (uint8_t)mn;
-      s_umx[r][c] = (uint8_t)mx;
-    }
-#pragma unroll
-    for (int k = 0; k < kWinPer; k++) {
-      const int t = tid + NT * k, r = min(t / kWin, kHR - 1), j = t % kWin;
-      const uint32_t* row = s_thr_stage + (r + 7) * kStageDw;
-      dw4[k] = __builtin_amdgcn_alignbyte(row[2 + j], row[1 + j], 3);
-    }
-    thr_sync<true>();  // every staged sample read: the next tile's DMA may land
-    if (has_next) thr_stage_issue(b, g, nb);
-    ph(1);
-  } else if constexpr (PRE >= 0) {
+  if constexpr (PRE >= 0) {
     const uint8_t* in = b.frames[f];
     uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
     uint8_t* decw = b.dec + (size_t)f * g.Wd * g.Hd;
@@ -630,7 +549,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
         *reinterpret_cast<uint32_t*>(&s_dec[r][4 * cc]) = y[0] | (y[2] << 8) | (y[4] << 16) | (y[6] << 24);
       }
     }
-    thr_sync<PIPE>();
+    __syncthreads();
     // tile min/max of every staged tile inside the image (whole tiles: W, H % 8 == 0)
     for (int i = tid; i < (kTH + 3) * (kTW + 4); i += NT) {
       const int r = i / (kTW + 4), c = i % (kTW + 4);
@@ -656,7 +575,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
       const int y = y0 - 1 + i / kHC, x = x0 - 1 + i % kHC;
       dv[k] = (i < kHR * kHC && y >= 0 && y < g.Hd && x >= 0 && x < g.Wd) ? s_dec[i / kHC + 7][i % kHC + 7] : 0;
     }
-    thr_sync<PIPE>();  // s_dec (over s_par) read before the labeling writes s_par
+    __syncthreads();  // s_dec (over s_par) read before the labeling writes s_par
   } else {
   // the tile's decimated pixels (+1 halo) are loaded together with the tile
   // min/max: one global round trip instead of two.  A window straddles two aligned
@@ -680,7 +599,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     s_umn[r][c] = in ? (uint8_t)(v & 0xff) : (uint8_t)255;
     s_umx[r][c] = in ? (uint8_t)(v >> 8) : (uint8_t)0;
   }
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(1);
   }
   // InternalBlockFilter: clipped 3x3 min of mins / max of maxes for tile rows ty0-1..ty0+kTH-1
@@ -697,7 +616,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     s_fmn[r][c] = mn;
     s_fmx[r][c] = mx;
   }
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(2);
   // InternalThreshold for the halo region; outside the image -> 127
   if constexpr (PRE < 0) {
@@ -749,7 +668,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   }
   }
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(3);
   // write this tile's threshold plane (4 bytes per thread)
   {
@@ -774,7 +693,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   const int pr = 2 * bty, pc = 2 * btx;
   const uint8_t a = T(pr, pc), bb = T(pr, pc + 1), c = T(pr + 1, pc), d = T(pr + 1, pc + 1);
   const uint32_t F = slot_of<TWD>(bty, btx, 0), L = slot_of<TWD>(bty, btx, 1), R = slot_of<TWD>(bty, btx, 2);
-  const uint32_t lane = (uint32_t)tid & 63u;
+  const uint32_t lane = lane_id();
   {
     const bool fg_left = btx > 0 && (a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255);
     const bool bg_left = btx > 0 && ((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0));
@@ -796,7 +715,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     s_par[F] = hF;
     s_par[L] = hL;
     s_par[R] = hR;
-    thr_sync<PIPE>();
+    __syncthreads();
   ph(4);
     // heads of the run(s) above this block's vertical links (read before any union)
     constexpr uint32_t kNone = 0xffffffffu;
@@ -811,7 +730,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     }
     // the left neighbour's targets (same wave: rows never straddle waves)
     const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
-    thr_sync<PIPE>();
+    __syncthreads();
   ph(5);
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
@@ -821,10 +740,10 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     if (tR != kNone && !(bg_in && tR == tL)) lds_union(s_par, hR, tR);
   }
 #undef T
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(6);
   const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(7);
   s_par[F] = rF;
   s_par[L] = rL;
@@ -859,7 +778,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   count(rF, nfg);
   count(rL, nbl);
   count(rR, nbr);
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(8);
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
@@ -880,7 +799,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     if (lF) s_li[F] = (uint16_t)iF;
     if (lL) s_li[L] = (uint16_t)iL;
     if (lR) s_li[R] = (uint16_t)iR;
-    thr_sync<PIPE>();  // (the descriptor below reads other threads' roots' slots)
+    __syncthreads();  // (the descriptor below reads other threads' roots' slots)
   }
   const size_t tl = (size_t)f * g.CTX * g.CTY + bi.y * g.CTX + bi.x;
   if (inimg) {
@@ -957,45 +876,17 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
           s_t[r][c] | (s_t[r + 1][c] << 8) | (s_t[r + 2][c] << 16) | ((uint32_t)s_t[r + 3][c] << 24);
     }
   }
-  thr_sync<PIPE>();
+  __syncthreads();
   ph(9);
   if (tid == 0) {
     b.nlroot[(size_t)f * g.CTX * g.CTY + bi.y * g.CTX + bi.x] = s_nlr;
-    if constexpr (!PIPE) kt_end(b, 1);
+    kt_end(b, 1);
   }
 }
 
 template <int TWD, int PRE>
 __global__ __launch_bounds__(CclTile<TWD>::NT) __attribute__((amdgpu_num_sgpr(AT_THR_SGPRS))) void k_thr_ccl(DevBufs b, Geom g, Params prm) {
-  thr_ccl_tile<TWD, PRE, false>(b, g, prm, xcd_block<AT_XCD_THR>(), false, TileIdx{0, 0, 0});
-}
-
-// Throughput mode, software-pipelined: a persistent grid (4 workgroups per CU, a
-// multiple of 8) walks the batch's tiles; the workgroups dealt to XCD k (blocks
-// b = k mod 8) take the k-th contiguous eighth of the (frame, tile row, tile column)
-// order, each workgroup every (grid / 8)-th tile of it.  The next tile's samples are
-// DMA'd into LDS while this one is labeled, so the tile's global round trip leaves the
-// workgroup's critical path (k_thr_ccl: one round trip at the start of every tile).
-__global__ __launch_bounds__(CclTile<64>::NT) __attribute__((amdgpu_num_sgpr(AT_THR_SGPRS), amdgpu_waves_per_eu(8))) void k_thr_ccl_pipe(DevBufs b, Geom g, Params prm, int nframes) {
-  kt_begin(b, 1);
-  const uint32_t per_frame = (uint32_t)(g.CTX * g.CTY), T = per_frame * (uint32_t)nframes;
-  const uint32_t xcd = blockIdx.x & 7, per = gridDim.x >> 3, q = T >> 3, rr = T & 7;
-  const uint32_t r0 = xcd * q + min(xcd, rr), r1 = r0 + q + (xcd < rr ? 1u : 0u);
-  auto tile = [&](uint32_t t) {
-    const uint32_t z = udiv24(t, per_frame), rem = t - z * per_frame, y = udiv24(rem, (uint32_t)g.CTX);
-    return TileIdx{(int)(rem - y * (uint32_t)g.CTX), (int)y, (int)z};
-  };
-  uint32_t t = r0 + (blockIdx.x >> 3);
-  if (t < r1) thr_stage_issue(b, g, tile(t));
-#pragma unroll 1
-  for (; t < r1; t += per) {
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's staging DMA (and stores) done
-    __syncthreads();                     // every wave's: the tile's samples are in LDS
-    const uint32_t tn = t + per;
-    thr_ccl_tile<64, -1, true>(b, g, prm, tile(t), tn < r1, tile(tn < r1 ? tn : t));
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) kt_end(b, 1);
+  thr_ccl_tile<TWD, PRE>(b, g, prm, xcd_block<AT_XCD_THR>());
 }
 
 // ---------------------------------------------------------------------------
@@ -3859,6 +3750,9 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 #define AT_EXT_U 4
 #endif
   constexpr int U = AT_EXT_U;
+#ifndef AT_EXT_KEY_UNROLL
+#define AT_EXT_KEY_UNROLL 4
+#endif
   uint32_t kr[U];
   for (uint32_t base = 0; base < n; base += NT * U) {
     uint32_t kk[U];
@@ -3934,7 +3828,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
       gp[u] = (uint32_t)dec[at - 1] | ((uint32_t)dec[at + 1] << 8) | ((uint32_t)dec[at - g.Wd] << 16) |
               ((uint32_t)dec[at + g.Wd] << 24);
     }
-#pragma unroll
+#pragma unroll AT_EXT_KEY_UNROLL
     for (int u = 0; u < U; u++) {
       const uint32_t t = base + u * NT + tid;
       if (t >= n) continue;
@@ -4502,7 +4396,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
         }
         const double Ex = Mx / N, Ey = My / N;
         const double Cxx = Mxx / N - Ex * Ex, Cxy = Mxy / N - Ex * Ey, Cyy = Myy / N - Ey * Ey;
-        const double nt = .5 * (double)det_atan2f((float)(-2 * Cxy), (float)(Cyy - Cxx));
+        const double nt = .5 * (double)det_atan2f_call((float)(-2 * Cxy), (float)(Cyy - Cxx));
         S.lines[tid][0] = Ex;
         S.lines[tid][1] = Ey;
         S.lines[tid][2] = (double)det_cosf((float)nt);
@@ -5081,12 +4975,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     dim3 grd(g.CTX, g.CTY, B);
     tk(1, st, 0);
     if (!on(1)) {}
-    else if (g.ctw != 32 && AT_THR_PIPE) {
-      // persistent, 4 workgroups per CU (nblobwg = 2 per CU), a multiple of 8 (XCD groups)
-      const uint32_t tiles = (uint32_t)(g.CTX * g.CTY * B);
-      const uint32_t grid = std::max(8u, std::min((uint32_t)(2 * nblobwg), tiles) & ~7u);
-      hipLaunchKernelGGL(k_thr_ccl_pipe, dim3(grid), dim3(CclTile<64>::NT), 0, st, b, g, prm, B);
-    } else if (g.ctw != 32) hipLaunchKernelGGL((k_thr_ccl<64, -1>), grd, dim3(CclTile<64>::NT), 0, st, b, g, prm);
+    else if (g.ctw != 32) hipLaunchKernelGGL((k_thr_ccl<64, -1>), grd, dim3(CclTile<64>::NT), 0, st, b, g, prm);
     else if (fmt == 0) hipLaunchKernelGGL((k_thr_ccl<32, 0>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
     else if (fmt == 1) hipLaunchKernelGGL((k_thr_ccl<32, 1>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
     else hipLaunchKernelGGL((k_thr_ccl<32, 2>), grd, dim3(CclTile<32>::NT), 0, st, b, g, prm);
