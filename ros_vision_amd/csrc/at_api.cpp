@@ -115,7 +115,8 @@ using namespace at;
 enum { kCtlNpts, kCtlNpairs, kCtlNdets, kCtlNquads, kCtlStatus, kCtlNpent, kCtlNqcand, kCtlCclOvf, kCtlNlr,
        kCtlPerFrame };
 enum { kCtlWorkhead = 0, kCtlQhead = 1, kCtlWorkheadSmall = 2, kCtlBlobPts = 3, kCtlNcls = 5,
-       kCtlDetHead = kCtlNcls + kNumCls, kCtlDecDone = kCtlDetHead + 1, kCtlScalars = kCtlDecDone + 1 };
+       kCtlDetHead = kCtlNcls + kNumCls, kCtlDecDone = kCtlDetHead + 1, kCtlWorkheadMid = kCtlDecDone + 1,
+       kCtlScalars = kCtlWorkheadMid + 1 };
 
 static constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 
@@ -468,6 +469,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.workhead = sc + kCtlWorkhead;
   b.qhead = sc + kCtlQhead;
   b.workhead_small = sc + kCtlWorkheadSmall;
+  b.workhead_mid = sc + kCtlWorkheadMid;
   b.blob_pts = sc + kCtlBlobPts;
   b.ncls = sc + kCtlNcls;
   b.det_head = sc + kCtlDetHead;
@@ -480,7 +482,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.qcand_cap = (uint32_t)(B * kQuadCandPerFrame);
   b.qcand = (QuadCand*)dalloc((size_t)b.qcand_cap * sizeof(QuadCand));
   // overflow area for the peak keys of pathological large blobs (one per large-blob team)
-  b.s_pk = (uint64_t*)dalloc((size_t)d->nblobwg * (kSortCap / 2) * 8);
+  b.s_pk = (uint64_t*)dalloc((size_t)2 * d->nblobwg * (kSortCap / 2) * 8);  // a slot per team (<= 2 nblobwg teams)
   // refine samples past LDS, one region per k_decode workgroup of the grid
   // launch_pipeline uses for a full batch (decode_grid)
   b.rsamp = (double*)dalloc((size_t)decode_grid(d->nblobwg, d->B) * 2 * (kMaxRefineSamples - kLdsRefine) * 8);

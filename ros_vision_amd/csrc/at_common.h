@@ -284,7 +284,8 @@ struct DevBufs {
   uint32_t* workhead; // [1]
   uint64_t* probe;    // [kProbeWords] phase clock stamps (diagnostics)
   uint32_t* blob_pts;       // [2] points processed by the small / large blob kernels (batch statistics)
-  uint32_t* workhead_small; // [1]
+  uint32_t* workhead_small; // [1] dequeue head of the stage's second large-blob launch
+  uint32_t* workhead_mid;   // [1] ... and of its third
   uint32_t* nqcand;   // [B] accepted quads queued for decode, per frame (qcand[f][kQuadCandPerFrame])
   uint32_t* qhead;    // [1]
   QuadCand* qcand;    // [qcand_cap]

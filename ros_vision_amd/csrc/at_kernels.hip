@@ -2537,7 +2537,9 @@ __device__ __forceinline__ float window_err(const Mom6& s, int32_t N) {
 // peak keys and the 90 segment fits of FitQuads.
 
 template <int NT, int CAP>
-constexpr int kKeySlots = (NT >= 512 && CAP <= 4096) ? 2 * CAP : CAP;  // latency-mode teams: bucket scatter room for CAP keys
+constexpr int kKeySlots = (NT >= 512 && CAP <= 4096) ? 2 * CAP  // latency-mode teams: bucket scatter room for CAP keys
+                          : CAP < 400 ? 400                      // (SegFits lives over the keys: 3.2 KB)
+                                      : CAP;
 
 // the 90 distinct segment fits of FitQuads: [a][b], a < b forward pi[a]->pi[b],
 // a > b wrap-around pi[a]->pi[b] (the closing side m3->m0).  They live over the
@@ -3921,17 +3923,19 @@ __device__ __forceinline__ void probe_flush(const DevBufs& b, const Params& prm,
 // is cheap); `slot` indexes the team's global sort scratch.
 template <int NT, int CAP, bool FUSE>
 __device__ __forceinline__ void large_blob_loop(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S,
-                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t nlo, uint32_t slot) {
+                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t nlo, uint32_t slot,
+                                int c0, int c1, int launch) {
   const int tid = threadIdx.x;
   uint32_t* pacc = S.pacc;
   if (tid < 22) pacc[tid] = 0;
   if (tid == 0) S.slow_dt = 0;
   uint64_t* gpk = b.s_pk + (size_t)slot * (kSortCap / 2);
   __syncthreads();
-  const int ncls = nlo ? 1 : g.nlarge;  // (blobs over 4096 points are all in class 0)
+  // size classes c0 .. c1-1 (blobs over 4096 points are all in class 0); every launch
+  // of the stage dequeues from its own head
   uint32_t nwork = 0;
-  for (int c = 0; c < ncls; c++) nwork += s_cnt[c];
-  uint32_t* head = nlo ? b.workhead_small : b.workhead;
+  for (int c = c0; c < c1; c++) nwork += s_cnt[c];
+  uint32_t* head = launch == 0 ? b.workhead : launch == 1 ? b.workhead_small : b.workhead_mid;
   while (true) {
     if (tid == 0) S.item = atomicAdd(head, 1u);
     __syncthreads();
@@ -3939,7 +3943,7 @@ __device__ __forceinline__ void large_blob_loop(const DevBufs& b, const Geom& g,
     __syncthreads();
     if (item >= nwork) break;
     uint32_t w = 0;
-    work_item(b, s_cnt, 0, ncls, item, &w);
+    work_item(b, s_cnt, c0, c1, item, &w);
     const PairInfo pi = FUSE ? PairInfo{b.pair_cnt[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], b.pair_off[(size_t)(w >> 16) * kMaxPairs + (w & 0xffff)], 0u} : load_pair_info(b, w);
     if (pi.n > (uint32_t)CAP || pi.n <= nlo) continue;  // the other launch's item (uniform)
     blob_item<NT, CAP, FUSE>(b, g, prm, S, gpk, s_combo, w, pi, pacc);
@@ -3957,29 +3961,30 @@ __device__ __forceinline__ void large_blob_loop(const DevBufs& b, const Geom& g,
 // small blob serialized every wave of the chip behind that address).  Software
 // pipeline: the work entry two items ahead and the pair-table entries one item
 // ahead are in flight while a blob is processed.
-template <bool FUSE>
-__device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<64, kSmallBlob>& S,
-                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t wv, uint32_t nwaves) {
+template <bool FUSE, int CAP = kSmallBlob>
+__device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<64, CAP>& S,
+                                const uint32_t* s_combo, const uint32_t* s_cnt, uint32_t wv, uint32_t nwaves,
+                                int c0, int c1) {
   const uint32_t lane = lane_id();
   uint32_t* pacc = S.pacc;
   if (lane < 22) pacc[lane] = 0;
   if (lane == 0) S.slow_dt = 0;
   uint32_t nwork = 0;
-  for (int c = g.nlarge; c < kNumCls; c++) nwork += s_cnt[c];
+  for (int c = c0; c < c1; c++) nwork += s_cnt[c];
   uint32_t item = wv;
   uint32_t w = 0, w1 = 0;
   PairInfo pi = {0, 0, 0};
   if (item < nwork) {
-    work_item(b, s_cnt, g.nlarge, kNumCls, item, &w);
+    work_item(b, s_cnt, c0, c1, item, &w);
     pi = load_pair_info(b, w);
   }
-  if (item + nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + nwaves, &w1);
+  if (item + nwaves < nwork) work_item(b, s_cnt, c0, c1, item + nwaves, &w1);
   for (; item < nwork; item += nwaves) {
     const bool has1 = item + nwaves < nwork;
     const PairInfo pi1 = has1 ? load_pair_info(b, w1) : PairInfo{0, 0, 0};
     uint32_t w2 = 0;
-    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, g.nlarge, kNumCls, item + 2 * nwaves, &w2);
-    [[clang::always_inline]] blob_item<64, kSmallBlob, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
+    if (item + 2 * nwaves < nwork) work_item(b, s_cnt, c0, c1, item + 2 * nwaves, &w2);
+    [[clang::always_inline]] blob_item<64, CAP, FUSE>(b, g, prm, S, nullptr, s_combo, w, pi, pacc);
     w = w1;
     pi = pi1;
     w1 = w2;
@@ -3997,8 +4002,14 @@ __device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g,
 // 8192 (86 KB, one workgroup per CU) over the few larger ones (nlo = 4096,
 // size class 0 only, its own dequeue head), instead of every large blob in
 // the 86 KB kernel.
+#ifndef AT_MID_BLOB
+#define AT_MID_BLOB 1
+#endif
+#ifndef AT_MID2_NT
+#define AT_MID2_NT 256
+#endif
 template <int NT, int CAP, bool FUSE = false>
-__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo) {
+__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo, int c0, int c1, int launch) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
   // device-clock span: the first launch's workgroups stamp their slots as usual; the
@@ -4006,7 +4017,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
   // the grid counter the first launch set), so the span covers both launches, as
   // the HIP events around the stage do
   uint32_t kt_slot = ~0u;
-  if (!nlo) {
+  if (!launch) {
     kt_begin(b, 9);
   } else if (b.kt_stage == 9 && tid == 0) {
     kt_slot = atomicAdd(b.kgrid, 1u);
@@ -4015,9 +4026,9 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, tid, NT);
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
-  large_blob_loop<NT, CAP, FUSE>(b, g, prm, S, s_combo, s_cnt, nlo, blockIdx.x);
-  if (tid == 0 && !nlo) kt_end(b, 9);
-  if (tid == 0 && nlo && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
+  large_blob_loop<NT, CAP, FUSE>(b, g, prm, S, s_combo, s_cnt, nlo, blockIdx.x, c0, c1, launch);
+  if (tid == 0 && !launch) kt_end(b, 9);
+  if (tid == 0 && launch && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
 }
 
 // K9a (small blobs, <= kSmallBlob points): one blob per wave, four independent
@@ -4026,19 +4037,32 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
 #ifndef AT_BS_WAVES
 #define AT_BS_WAVES 4
 #endif
-template <bool FUSE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : AT_BS_WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm) {
-  __shared__ BlobShared<64, kSmallBlob> Ss[4];
+
+// Classes c0 .. c1-1 of blobs of up to CAP points; `launch` > 0: not the stage's first
+// launch (appends its device-clock stamps).  (A CAP-128 launch for the blobs of up to
+// 128 points kept 123 VGPRs -- the per-blob fits, not the per-point arrays, set the
+// register count -- so the small blobs stay in one CAP-512 launch.)
+template <bool FUSE, int CAP = kSmallBlob, int WAVES = AT_BS_WAVES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm,
+                                                                                                         int c0, int c1, int launch) {
+  __shared__ BlobShared<64, CAP> Ss[4];
   const int wave = threadIdx.x >> 6;
-  kt_begin(b, 8);
+  uint32_t kt_slot = ~0u;
+  if (!launch) {
+    kt_begin(b, 8);
+  } else if (b.kt_stage == 8 && threadIdx.x == 0) {
+    kt_slot = atomicAdd(b.kgrid, 1u);
+    if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
+  }
   __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
   load_combos(s_combo, threadIdx.x, 256);
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
   __syncthreads();
-  small_blob_loop<FUSE>(b, g, prm, Ss[wave], s_combo, s_cnt, blockIdx.x * 4 + wave, gridDim.x * 4);
+  small_blob_loop<FUSE, CAP>(b, g, prm, Ss[wave], s_combo, s_cnt, blockIdx.x * 4 + wave, gridDim.x * 4, c0, c1);
   if (b.kt_stage == 8) {  // (uniform: the timed launch only)
     __syncthreads();
-    if (threadIdx.x == 0) kt_end(b, 8);
+    if (threadIdx.x == 0 && !launch) kt_end(b, 8);
+    if (threadIdx.x == 0 && launch && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
   }
 }
 
@@ -4059,11 +4083,12 @@ __global__ __launch_bounds__(512) void k_blob_lat(DevBufs b, Geom g, Params prm)
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
   const uint32_t team = blockIdx.x >> 1, nteam = gridDim.x >> 1;
   if ((blockIdx.x & 1) == 0) {
-    large_blob_loop<512, 4096, true>(b, g, prm, *reinterpret_cast<SL*>(s_raw), s_combo, s_cnt, 0u, team);
+    large_blob_loop<512, 4096, true>(b, g, prm, *reinterpret_cast<SL*>(s_raw), s_combo, s_cnt, 0u, team, 0, g.nlarge, 0);
   } else {
     __syncthreads();
     const int wave = tid >> 6;
-    small_blob_loop<true>(b, g, prm, reinterpret_cast<SS*>(s_raw)[wave], s_combo, s_cnt, team * 8 + wave, nteam * 8);
+    small_blob_loop<true>(b, g, prm, reinterpret_cast<SS*>(s_raw)[wave], s_combo, s_cnt, team * 8 + wave, nteam * 8,
+                          g.nlarge, kNumCls);
   }
   if (b.kt_stage == 9) {  // (uniform: the timed launch only)
     __syncthreads();
@@ -5031,21 +5056,32 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     if (lat_fused) {  // latency mode: both blob kinds in one launch (no k_extents, no fork / join)
       hipLaunchKernelGGL(k_blob_lat, dim3(nblobwg), dim3(512), 0, s, b, g, prm);
     } else if (g.ctw == 32 && cap4k) {  // latency mode, timed apart: extents, SelectBlobs and keys in the team
-      hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
+      hipLaunchKernelGGL((k_blob<512, 4096, true>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
     } else if (B < kWideBlobMaxBatch || prm.wide_blob) {  // (latency: one launch, longest blob first)
-      if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
-      else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u);
+      if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
+      else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
+    } else if (cap4k && AT_MID_BLOB) {
+      // throughput: blobs of 1025-4096 points in 256-thread teams, the 513-1024-point
+      // class (two thirds of the large blobs at 720p) in 128-thread teams (CAP 1024:
+      // the same 8 points per thread as the one-wave kernel; barriers over two waves)
+      if (AT_MID_BLOB >= 2) {  // (experiment: 1025-2048 points in their own launch too)
+        hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, 1, 0);
+        hipLaunchKernelGGL((k_blob<AT_MID2_NT, 2048>), dim3(nblobwg * 256 / AT_MID2_NT), dim3(AT_MID2_NT), 0, s, b, g, prm, 0u, 1, 2, 2);
+      } else {
+        hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, 2, 0);
+      }
+      hipLaunchKernelGGL((k_blob<128, 1024>), dim3(2 * nblobwg), dim3(128), 0, s, b, g, prm, 0u, 2, 3, 1);
     } else {
-      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u);
-      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(256), 0, s, b, g, prm, 4096u);
+      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
+      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(256), 0, s, b, g, prm, 4096u, 0, 1, 1);
     }
     tk(9, s, 1);
   };
   auto blob_small = [&](hipStream_t s) {
     tk(8, s, 0);
     if (!on(8) || lat_fused) {}
-    else if (fuse_small) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm);
-    else hipLaunchKernelGGL(k_blob_small<false>, dim3(prm.sblob_wg ? prm.sblob_wg : nblobwg * 2), dim3(256), 0, s, b, g, prm);
+    else if (fuse_small) hipLaunchKernelGGL(k_blob_small<true>, dim3(nblobwg * 2), dim3(256), 0, s, b, g, prm, g.nlarge, kNumCls, 0);
+    else hipLaunchKernelGGL(k_blob_small<false>, dim3(prm.sblob_wg ? prm.sblob_wg : nblobwg * 2), dim3(256), 0, s, b, g, prm, g.nlarge, kNumCls, 0);
     tk(8, s, 1);
   };
   if (ev || !st2 || lat_fused) {
