@@ -22,7 +22,11 @@ NODE = os.path.join(ROOT, "node")
 
 @pytest.fixture(scope="module")
 def built():
-    subprocess.run(["make", "-C", NODE, "-s"], check=True)
+    import fcntl
+    # one make at a time (pytest-xdist workers share the tree)
+    with open(os.path.join(NODE, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", NODE, "-s"], check=True)
     return NODE
 
 
