@@ -1430,6 +1430,9 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 #else
 #define AT_BND_ATTR
 #endif
+#ifndef AT_BND_TWO
+#define AT_BND_TWO 1
+#endif
 // KEPT (throughput mode): the size test comes with the root word (k_ccl_merge);
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
@@ -1445,7 +1448,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   // threshold values with pixels of blobs under 25 pixels folded to 127: every
   // BlobDiff condition then reads one byte per neighbour (v0 + v1 == 255 holds
   // only when both blobs are kept; the dedup rule's "!= 127 and kept" likewise)
-  __shared__ uint8_t s_tthr[(4 * kBndRows + 1) * 66];
+  __shared__ __attribute__((aligned(4))) uint8_t s_tthr[(4 * kBndRows + 1) * 66];
   __shared__ uint32_t s_tlab[(4 * kBndRows + 1) * 66];
   const TileIdx bi = xcd_block<AT_XCD_BND>();
   const int f = bi.z;
@@ -1503,10 +1506,116 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     }
   }
   __syncthreads();  // LDS tables initialised
-  const int x = 1 + bi.x * 64 + threadIdx.x;
   const uint32_t lane = lane_id();
   const size_t tb = (size_t)f * g.ntb + bi.y * gridDim.x + bi.x;
   uint64_t* pts_out = b.pts + tb * g.bnd_region;
+#if AT_BND_TWO
+  // two horizontally adjacent pixels per lane, a wave over two tile rows per step
+  // (lanes 0-31 the upper row, 32-63 the lower): the wave-wide work of a step -- the
+  // point-offset scan, the pair runs, the staging atomic -- serves 128 pixels.  (Pair
+  // runs may continue from the upper row into the lower: only their counts are used.)
+  const int cx = 2 * (int)(lane & 31);  // tile column of the lane's first pixel
+  const int xa = 1 + bi.x * 64 + cx;    // its image column
+  for (int r = 0; r < kBndRows / 2; r++) {
+    const int ly = (r * 4 + threadIdx.y) * 2 + (int)(lane >> 5);  // tile row of the pixels
+    const int y = ty0 + ly;
+    // threshold bytes of halo columns cx .. cx+3 (left neighbour, the two pixels, right
+    // neighbour) in rows ly and ly + 1: four aligned 16-bit LDS reads
+    const int eb = ly * kTC + cx;
+    const uint32_t ra = (uint32_t)*reinterpret_cast<const uint16_t*>(s_tthr + eb) |
+                        ((uint32_t)*reinterpret_cast<const uint16_t*>(s_tthr + eb + 2) << 16);
+    const uint32_t rb = (uint32_t)*reinterpret_cast<const uint16_t*>(s_tthr + eb + kTC) |
+                        ((uint32_t)*reinterpret_cast<const uint16_t*>(s_tthr + eb + kTC + 2) << 16);
+    // the pixels' points: direction mask (bit 4j + dir for pixel j), neighbour labels
+    uint32_t hm = 0, nb[8], rep[2];
+    bool b2w[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      rep[j] = 0;
+      b2w[j] = false;
+#pragma unroll
+      for (int d = 0; d < 4; d++) nb[4 * j + d] = 0;
+      const uint32_t v0 = (ra >> (8 * j + 8)) & 0xff;
+      if (xa + j <= g.Wd - 2 && y <= g.Hd - 2 && v0 != 127) {
+        const uint32_t vl = (ra >> (8 * j)) & 0xff, vr = (ra >> (8 * j + 16)) & 0xff;
+        const uint32_t vdl = (rb >> (8 * j)) & 0xff, vd = (rb >> (8 * j + 8)) & 0xff, vdr = (rb >> (8 * j + 16)) & 0xff;
+        const int e0 = eb + j + 1, ed = e0 + kTC;
+        rep[j] = s_tlab[e0];
+        b2w[j] = v0 == 0;
+        if (v0 + vr == 255) { hm |= 1u << (4 * j); nb[4 * j] = s_tlab[e0 + 1]; }
+        if (v0 + vdr == 255) { hm |= 2u << (4 * j); nb[4 * j + 1] = s_tlab[ed + 1]; }
+        if (v0 + vd == 255) { hm |= 4u << (4 * j); nb[4 * j + 2] = s_tlab[ed]; }
+        const bool dedup = vl != 127 && vd != 127 && vd != vl && xa + j != 1;
+        if (!dedup && v0 + vdl == 255) { hm |= 8u << (4 * j); nb[4 * j + 3] = s_tlab[ed - 1]; }
+      }
+    }
+    // pair histogram: the lane's first pair with the count of its points in it (labels
+    // are < 2^20 -- decimated planes of at most 1024 x 1024 -- so label equality is
+    // key equality), runs of equal first pairs in consecutive lanes summed (wave scan),
+    // the rare other pairs of a lane one by one
+    const bool got = hm != 0;
+    const uint32_t rf = (hm & 0xfu) ? rep[0] : rep[1];
+    uint32_t nf = nb[7];
+#pragma unroll
+    for (int d = 6; d >= 0; d--) nf = ((hm >> d) & 1) ? nb[d] : nf;
+    uint32_t cnt = 0, xm = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+      const uint32_t rj = rep[d >> 2];
+      const bool in = (hm >> d) & 1, eq = (rj == rf && nb[d] == nf) || (rj == nf && nb[d] == rf);
+      cnt += in && eq;
+      xm |= (in && !eq) ? 1u << d : 0u;
+    }
+    // one scan for both: the first-pair counts (low half) and the lane's points (high)
+    const uint32_t npts = (uint32_t)__builtin_popcount(hm);
+    const uint32_t sc = wave_incl_scan(cnt | (npts << 16), AddOp(), 0u);
+    const uint32_t incl = sc & 0xffffu;
+    const uint32_t below = (sc >> 16) - npts, wtot = wave_read(sc, 63) >> 16;
+    const uint64_t kp = got ? make_qbp(rf, nf, 0, 0, 0, false) >> 24 : 0ull;
+    {
+      const uint64_t prev = wave_shr1_u64(kp);
+      const bool same = got && lane > 0 && prev == kp;
+      const uint64_t same_mask = __ballot(same);
+      const bool head = got && !same;
+      const uint32_t len = head ? run_len(same_mask, lane) : 1u;
+      const uint32_t incl_end = (uint32_t)__shfl((int)incl, (int)(lane + len - 1));
+      if (head) {
+        const uint32_t tot = incl_end - incl + cnt;
+        if (!lds_pair_add(s_pkey, s_pcnt, kp, tot)) {  // LDS table full
+          bnd_spill(b, f, kp, tot);
+          s_spill = 1;
+        }
+      }
+      if (__ballot(xm != 0)) {
+#pragma unroll
+        for (int d = 0; d < 8; d++) {
+          if ((xm >> d) & 1) {
+            const uint64_t k = make_qbp(rep[d >> 2], nb[d], 0, 0, 0, false) >> 24;
+            if (!lds_pair_add(s_pkey, s_pcnt, k, 1u)) {
+              bnd_spill(b, f, k, 1u);
+              s_spill = 1;
+            }
+          }
+        }
+      }
+    }
+    // wave-aggregated append of the points into the LDS staging buffer
+    uint32_t wbase = 0;
+    if (lane == 0 && wtot) wbase = atomicAdd(&s_npts, wtot);
+    wbase = __shfl(wbase, 0);
+    uint32_t pos = wbase + below;
+#pragma unroll
+    for (int d = 0; d < 8; d++)
+      if ((hm >> d) & 1) {
+        const uint64_t k = make_qbp(rep[d >> 2], nb[d], xa + (d >> 2), y, d & 3, b2w[d >> 2]);
+        if (pos < (uint32_t)kBndStage) s_pts[pos] = k;
+        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = k;
+        else atomicOr(b.status + f, kStatusPointsOverflow);
+        pos++;
+      }
+  }
+#else
+  const int x = 1 + bi.x * 64 + threadIdx.x;
   for (int r = 0; r < kBndRows; r++) {
     const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
     const int y = ty0 + ly;
@@ -1599,6 +1708,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
         pos++;
       }
   }
+#endif
   __syncthreads();
   // the tile's own regions: points and compacted pair entries, plain stores
   // (no per-frame counter: a device-scope atomic per tile on a per-frame
@@ -5039,8 +5149,9 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   // (latency mode: the blob kernels do k_extents' work themselves, up to 4096-point blobs)
   // latency mode: extents, SelectBlobs and keys inside the small-blob wave and (up to
   // 4096-point blobs) the 512-thread large-blob team.  (Throughput mode keeps
-  // k_extents: the fused small-blob kernel needs 2 waves/SIMD, or spills at 4, and
-  // measured 1-5 % slower in concurrent throughput, profiles/r03h, r03i.)
+  // k_extents: the fused small-blob kernel needs 2 waves/SIMD, or spills at 4: k_blob_small
+  // 0.37 -> 0.61 ms serialized and 5-7 % less concurrent throughput, 13 % with the large
+  // blobs fused too and no k_extents launch, profiles/r05_more/fuse_extents_ab_stages.txt)
   const bool fuse_small = g.ctw == 32;
   // latency mode with blobs of up to 4096 points: k_blob_lat holds both kinds (stage
   // profiling and the kernel timer keep the two kernels, to time them apart)
