@@ -368,6 +368,9 @@ __device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
 }
 // find with path halving: every visited node is pointed at its grandparent (an
 // ancestor with a smaller id, so the atomicMin never loses a link)
+#ifndef AT_CCL_LEAN_SYNC
+#define AT_CCL_LEAN_SYNC 1
+#endif
 __device__ __forceinline__ uint32_t lds_find(uint32_t* par, uint32_t n) {
   uint32_t p = lds_load(par + n);
   while (p != n) {
@@ -730,7 +733,11 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     }
     // the left neighbour's targets (same wave: rows never straddle waves)
     const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
-    __syncthreads();
+    // (no barrier before the unions: a target read while another block's union or path
+    // compression runs is a node of the same component -- unions and compressions only
+    // lower a parent within its component -- so the union it takes part in is still the
+    // right one; a changed value only defeats the left-neighbour dedup, an extra union)
+    if (!AT_CCL_LEAN_SYNC) __syncthreads();
   ph(5);
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
@@ -743,7 +750,10 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   __syncthreads();
   ph(6);
   const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
-  __syncthreads();
+  // (no barrier before the root writes: each writes a node's final root -- the smallest
+  // slot of its component, so a concurrent compression's atomicMin leaves it -- and a
+  // find that reads it lands on that root)
+  if (!AT_CCL_LEAN_SYNC) __syncthreads();
   ph(7);
   s_par[F] = rF;
   s_par[L] = rL;
@@ -1506,6 +1516,12 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     }
   }
   __syncthreads();  // LDS tables initialised
+#ifdef AT_BND_CUT  // (diagnostic builds: the staging alone / without the output phase)
+  if (AT_BND_CUT == 1) {
+    if (tid == 0) { b.tcnt[(size_t)f * g.ntb + bi.y * gridDim.x + bi.x] = 0; b.tent[(size_t)f * g.ntb + bi.y * gridDim.x + bi.x] = 0; kt_end(b, 4); }
+    return;
+  }
+#endif
   const uint32_t lane = lane_id();
   const size_t tb = (size_t)f * g.ntb + bi.y * gridDim.x + bi.x;
   uint64_t* pts_out = b.pts + tb * g.bnd_region;
@@ -1710,6 +1726,12 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
   }
 #endif
   __syncthreads();
+#ifdef AT_BND_CUT
+  if (AT_BND_CUT == 2) {
+    if (tid == 0) { b.tcnt[tb] = 0; b.tent[tb] = 0; kt_end(b, 4); }
+    return;
+  }
+#endif
   // the tile's own regions: points and compacted pair entries, plain stores
   // (no per-frame counter: a device-scope atomic per tile on a per-frame
   // address serialized the tiles of a frame)

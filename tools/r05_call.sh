@@ -3,6 +3,7 @@
 #   BENCH=1      the default bench line -> bench.json
 #   LIBS="a.so b.so"     interleaved concurrent A/B (tools/ab_stages.sh)
 #   PMCLIBS="a.so b.so"  FETCH / WRITE bytes per kernel of each library (tools/pmc_ab.sh)
+#   LDSLIBS="a.so b.so"  LDS instructions, bank conflicts, wave-cycles per kernel of each library
 #   ISO=1        bench.py --isolated-only under rocprofv3 --kernel-trace --stats, roofline_check
 #   SQX=1        per-class VALU counter passes + tools/valu_rates (issue costs)
 # usage: TAG=r05b GPU_TESTS=1 ... bash tools/r05_call.sh
@@ -28,6 +29,15 @@ if [ -n "${TIMER_AB:-}" ]; then  # the timed region with and without the live ke
 fi
 if [ -n "${LIBS:-}" ]; then TAG=$TAG bash tools/ab_stages.sh > /dev/null || exit 1; fi
 if [ -n "${PMCLIBS:-}" ]; then LIBS="$PMCLIBS" TAG=$TAG/pmc bash tools/pmc_ab.sh > $O/pmc_ab.txt 2> $O/pmc_ab.err || exit 1; fi
+if [ -n "${LDSLIBS:-}" ]; then  # LDS instructions / bank conflicts / wave-cycles per kernel of each library
+  SHORTL="$R/bench.py --no-cpu-baseline --no-stage-profile --batch 192 --steps 4 --warmup 1 --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --isolated-batches 0"
+  for lib in $LDSLIBS; do
+    n=$(basename $lib .so)
+    (cd /tmp && AT_HIP_LIB=$R/$lib timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY \
+       --output-format csv -d $R/$O/lds_$n -o run -- python3 $SHORTL > /dev/null 2> $R/$O/lds_$n.err) || exit 1
+    python3 tools/pmc_agg.py $O/lds_$n/run_counter_collection.csv > $O/lds_$n.txt
+  done
+fi
 if [ -n "${ISO:-}" ]; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/trace_iso -o run -- \
      python3 $R/bench.py --isolated-only > $R/$O/iso_traced.json 2> $R/$O/iso_traced.err) || exit 1
