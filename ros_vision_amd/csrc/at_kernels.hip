@@ -1378,8 +1378,19 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 }
 
 
+// slot hash of a pair key in the tile's LDS table: the low word (the smaller label and
+// 12 bits of the larger) times a 32-bit golden-ratio constant, top 9 bits -- one
+// v_mul_lo_u32 instead of the 64-bit product (AT_BND_HASH32=0: the frame table's hash)
+#ifndef AT_BND_HASH32
+#define AT_BND_HASH32 1
+#endif
+__device__ __forceinline__ uint32_t pair_hash(uint64_t key) {
+  static_assert(kLdsPairSlots == 512, "9-bit slot hash");
+  if (AT_BND_HASH32) return ((uint32_t)key * 0x9E3779B1u) >> 23;
+  return (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
+}
 __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uint64_t key, uint32_t len) {
-  uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
+  uint32_t h = pair_hash(key);
   for (int probe = 0; probe < kLdsPairSlots; probe++) {
     const uint64_t k = keys[h];
     if (k == key) {
@@ -1400,7 +1411,7 @@ __device__ __forceinline__ bool lds_pair_add(uint64_t* keys, uint32_t* cnts, uin
 
 // slot of a key already in the tile's LDS pair table
 __device__ __forceinline__ uint32_t lds_pair_slot(const uint64_t* keys, uint64_t key) {
-  uint32_t h = (uint32_t)(mix_hash(key) & (kLdsPairSlots - 1));
+  uint32_t h = pair_hash(key);
   while (keys[h] != key) h = (h + 1) & (kLdsPairSlots - 1);
   return h;
 }
