@@ -633,17 +633,27 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
         if (y >= 0 && y < g.Hd) {
           const int fr = (y >> 2) - (ty0 - 1);
           const int mn0 = s_fmn[fr][j], mx0 = s_fmx[fr][j], mn1 = s_fmn[fr][j + 1], mx1 = s_fmx[fr][j + 1];
-          const bool ok0 = mx0 - mn0 >= prm.min_white_black_diff, ok1 = mx1 - mn1 >= prm.min_white_black_diff;
-          const uint32_t th0 = (uint32_t)(mn0 + (mx0 - mn0) / 2), th1 = (uint32_t)(mn1 + (mx1 - mn1) / 2);
-          out = 0;
+          const int d0 = mx0 - mn0, d1 = mx1 - mn1;
+          // (d < 0 only where every tile of the 3x3 is outside the image: its bytes are
+          // outside too, 127 below whatever th is)
+          const uint32_t th0 = (uint32_t)(mn0 + (d0 >> 1)), th1 = (uint32_t)(mn1 + (d1 >> 1));
+          // v > th for the four bytes at once, in 16-bit lanes (bytes 0 and 2, bytes 1 and
+          // 3): bit 8 of th + 0x100 - v (in 1 .. 0x1ff, no borrow between lanes) is clear
+          // exactly when v > th
+          const uint32_t wv = dw4[k];
+          const uint32_t glo = ~((th0 | (th1 << 16)) + 0x01000100u - (wv & 0x00ff00ffu)) & 0x01000100u;
+          const uint32_t ghi = ~((th1 | (th1 << 16)) + 0x01000100u - ((wv >> 8) & 0x00ff00ffu)) & 0x01000100u;
+          out = ((glo >> 8) * 0xffu) | (((ghi >> 8) * 0xffu) << 8);
+          // 127 where the tile's contrast is too low (byte 0: column j, bytes 1-3: j + 1)
+          // or the byte lies outside the image (the windows at the left / right border)
+          uint32_t bad = (d0 >= prm.min_white_black_diff ? 0u : 0xffu) | (d1 >= prm.min_white_black_diff ? 0u : 0xffffff00u);
+          const int xs = x0 - 1 + 4 * j;
+          if (xs < 0 || xs + 3 >= g.Wd) {
 #pragma unroll
-          for (int bb = 0; bb < 4; bb++) {
-            const int x = x0 - 1 + 4 * j + bb;
-            const bool ok = bb == 0 ? ok0 : ok1;
-            const uint32_t v = (dw4[k] >> (8 * bb)) & 0xffu, th = bb == 0 ? th0 : th1;
-            const uint32_t res = (x < 0 || x >= g.Wd || !ok) ? 127u : (v > th ? 255u : 0u);
-            out |= res << (8 * bb);
+            for (int bb = 0; bb < 4; bb++)
+              if (xs + bb < 0 || xs + bb >= g.Wd) bad |= 0xffu << (8 * bb);
           }
+          out = (out & ~bad) | (0x7f7f7f7fu & bad);
         }
         *reinterpret_cast<uint32_t*>(&s_t[r][4 * j]) = out;
       }
