@@ -4710,19 +4710,29 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
     // sharpen (apriltag.c) over the total_width^2 grid: each lane owns cells t, t+64, t+128
     constexpr int kShR = (kMaxTotalWidth * kMaxTotalWidth + kDecodeThreads - 1) / kDecodeThreads;
     double shv[kShR];
+    // (the lane's cell indices recomputed per quad: hoisted out of the item loop they
+    // were spilled to scratch and reloaded here, one round trip each)
+    int tl = tid;
+    __asm__ volatile("" : "+v"(tl));
 #pragma unroll
     for (int r = 0; r < kShR; r++) {
-      const int t = tid + 64 * r;
+      const int t = tl + 64 * r;
       shv[r] = 0;
       if (t < tw * tw) {
+        // the kernel {0,-1,0; -1,4,-1; 0,-1,0} in the reference's tap order, its zero taps
+        // left out: they add +-0, which changes no nonzero partial sum, and the sign of a
+        // zero sum reaches no decision (a value is never -0: v - m is +0 when v == m).
+        // The five reads are issued together (the 3x3 loop's reads went one at a time,
+        // their addresses spilled to scratch)
         const int y = t / tw, x = t % tw;
-        const double kern[9] = {0, -1, 0, -1, 4, -1, 0, -1, 0};
+        const double up = S.values[y > 0 ? t - tw : t], left = S.values[x > 0 ? t - 1 : t], c = S.values[t];
+        const double right = S.values[x < tw - 1 ? t + 1 : t], down = S.values[y < tw - 1 ? t + tw : t];
         double acc = 0;
-        for (int i = 0; i < 3; i++)
-          for (int j = 0; j < 3; j++) {
-            if ((y + i - 1) < 0 || (y + i - 1) > tw - 1 || (x + j - 1) < 0 || (x + j - 1) > tw - 1) continue;
-            acc += S.values[(y + i - 1) * tw + (x + j - 1)] * kern[i * 3 + j];
-          }
+        if (y > 0) acc = acc - up;
+        if (x > 0) acc = acc - left;
+        acc = acc + c * 4;
+        if (x < tw - 1) acc = acc - right;
+        if (y < tw - 1) acc = acc - down;
         shv[r] = acc;
       }
     }
@@ -4756,15 +4766,26 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
       r[0] = rcode0;
 #pragma unroll
       for (int k = 1; k < 4; k++) r[k] = rotate90_n(r[k - 1], nbits);
-      for (int ent = tid; ent < prm.fam.ncodes; ent += kDecodeThreads) {
-        // the codebook straight from HBM (L2-resident: every workgroup reads the same
-        // table; an LDS copy cost 8 KB per one-wave workgroup, and the LDS freed lets
-        // the concurrent batches' kernels co-reside: +2.8 % throughput, profiles/r03l)
-        const uint64_t c = b.book_code[ent];
+      // the codebook straight from HBM (L2-resident: every workgroup reads the same
+      // table; an LDS copy cost 8 KB per one-wave workgroup, and the LDS freed lets
+      // the concurrent batches' kernels co-reside: +2.8 % throughput, profiles/r03l),
+      // four of a lane's entries loaded together (tag36h11: 3 round trips instead of 10)
+      constexpr int kBookChunk = 4;
+      for (int e0 = 0; e0 < prm.fam.ncodes; e0 += kBookChunk * kDecodeThreads) {
+        uint64_t cw[kBookChunk];
 #pragma unroll
-        for (int rot = 0; rot < 4; rot++) {
-          const int hd = __popcll(r[rot] ^ c);
-          if (hd <= 2) bc = min(bc, (uint32_t)((rot << 24) | (hd << 16) | ent));
+        for (int k = 0; k < kBookChunk; k++) {
+          const int ent = e0 + tid + kDecodeThreads * k;
+          cw[k] = ent < prm.fam.ncodes ? b.book_code[ent] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kBookChunk; k++) {
+          const int ent = e0 + tid + kDecodeThreads * k;
+#pragma unroll
+          for (int rot = 0; rot < 4; rot++) {
+            const int hd = __popcll(r[rot] ^ cw[k]);
+            if (ent < prm.fam.ncodes && hd <= 2) bc = min(bc, (uint32_t)((rot << 24) | (hd << 16) | ent));
+          }
         }
       }
 #pragma unroll
