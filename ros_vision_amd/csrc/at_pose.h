@@ -305,6 +305,19 @@ __device__ __forceinline__ double polyval(const double* p, int degree, double x)
   return ret;
 }
 
+// Element i (0 .. 3) of a 4-entry local array, read or written by selects over the
+// four static slots: a lane-varying or runtime index into a private array otherwise
+// keeps the array in scratch memory (a global-memory round trip per access)
+__device__ __forceinline__ double pick4(const double* a, int i) {
+  return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
+}
+__device__ __forceinline__ void put4(double* a, int i, double v) {
+  a[0] = i == 0 ? v : a[0];
+  a[1] = i == 1 ? v : a[1];
+  a[2] = i == 2 ? v : a[2];
+  a[3] = i == 3 ? v : a[3];
+}
+
 // Four lanes (a DPP quad) work on one detection: every quantity is computed
 // redundantly on all four, except the root brackets of solve_poly_approx, which
 // are independent and are solved one per lane; the roots are then gathered in
@@ -329,7 +342,8 @@ __device__ __forceinline__ int quad_bcast(int v) {
 // (nor, by Gauss-Lucas, a derivative root), so the sign test and the bracketed
 // root are unchanged while the safeguarded Newton needs far fewer steps.
 // Bracket `sub` (<= n_der <= 3) is this lane's; the caller's quad supplies the rest.
-__device__ int solve_poly_level(const double* p, int degree, const double* der_roots, int n_der, double* roots,
+// (der_roots and roots: 4-entry arrays, indexed through pick4 / put4)
+__device__ __forceinline__ int solve_poly_level(const double* p, int degree, const double* der_roots, int n_der, double* roots,
                                 int sub) {
   double MAX_ROOT = 1000;
   if (p[degree] != 0) {
@@ -343,8 +357,8 @@ __device__ int solve_poly_level(const double* p, int degree, const double* der_r
   int my_has = 0;
   if (sub <= n_der) {
     const int i = sub;
-    const double mn = i == 0 ? -MAX_ROOT : der_roots[i - 1];
-    const double mx = i == n_der ? MAX_ROOT : der_roots[i];
+    const double mn = i == 0 ? -MAX_ROOT : pick4(der_roots, i - 1);
+    const double mx = i == n_der ? MAX_ROOT : pick4(der_roots, i);
     const double fmn = polyval(p, degree, mn), fmx = polyval(p, degree, mx);
     if (fmn * fmx < 0) {
       double lower, upper;
@@ -384,13 +398,13 @@ __device__ int solve_poly_level(const double* p, int degree, const double* der_r
   int n = 0;
   double r;
   r = quad_bcast<0>(my_root);
-  if (quad_bcast<0>(my_has)) roots[n++] = r;
+  if (quad_bcast<0>(my_has)) put4(roots, n++, r);
   r = quad_bcast<1>(my_root);
-  if (quad_bcast<1>(my_has)) roots[n++] = r;
+  if (quad_bcast<1>(my_has)) put4(roots, n++, r);
   r = quad_bcast<2>(my_root);
-  if (quad_bcast<2>(my_has)) roots[n++] = r;
+  if (quad_bcast<2>(my_has)) put4(roots, n++, r);
   r = quad_bcast<3>(my_root);
-  if (quad_bcast<3>(my_has)) roots[n++] = r;
+  if (quad_bcast<3>(my_has)) put4(roots, n++, r);
   return n;
 }
 
@@ -410,7 +424,7 @@ __device__ __forceinline__ double horner(const double* p, int degree, double x) 
   return r;
 }
 // This lane's bracket root (my_has: one exists); the caller gathers.
-__device__ void solve_poly_level_wave_lane(const double* p, int degree, const double* der_roots, int n_der,
+__device__ __forceinline__ void solve_poly_level_wave_lane(const double* p, int degree, const double* der_roots, int n_der,
                                            double& my_root, int& my_has) {
   double MAX_ROOT = 1000;
   if (p[degree] != 0) {
@@ -424,8 +438,8 @@ __device__ void solve_poly_level_wave_lane(const double* p, int degree, const do
   my_root = 0;
   my_has = 0;
   if (sub <= n_der) {
-    const double mn = sub == 0 ? -MAX_ROOT : der_roots[sub - 1];
-    const double mx = sub == n_der ? MAX_ROOT : der_roots[sub];
+    const double mn = sub == 0 ? -MAX_ROOT : pick4(der_roots, sub - 1);
+    const double mx = sub == n_der ? MAX_ROOT : pick4(der_roots, sub);
     const double fmn = polyval(p, degree, mn), fmx = polyval(p, degree, mx);
     if (fmn * fmx < 0) {
       double lower = fmn < fmx ? mn : mx, upper = fmn < fmx ? mx : mn;
@@ -483,7 +497,7 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
   return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
 }
-__device__ int solve_poly_level_wave(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
+__device__ __forceinline__ int solve_poly_level_wave(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
   double my_root;
   int my_has;
   solve_poly_level_wave_lane(p, degree, der_roots, n_der, my_root, my_has);
@@ -491,19 +505,19 @@ __device__ int solve_poly_level_wave(const double* p, int degree, const double* 
 #pragma unroll
   for (int s2 = 0; s2 < 4; s2++) {
     const double r = readlane_f64(my_root, 16 * s2);
-    if (__builtin_amdgcn_readlane(my_has, 16 * s2)) roots[n++] = r;
+    if (__builtin_amdgcn_readlane(my_has, 16 * s2)) put4(roots, n++, r);
   }
   return n;
 }
 
 template <bool WAVE>
-__device__ int solve_quartic_approx(const double* p4, double* roots, int sub) {
+__device__ __forceinline__ int solve_quartic_approx(const double* p4, double* roots, int sub) {
   // derivative chain: p4 (deg 4) -> p3 -> p2 -> p1 (linear)
   double d3[4], d2[3], d1[2];
   for (int i = 0; i < 4; i++) d3[i] = (i + 1) * p4[i + 1];
   for (int i = 0; i < 3; i++) d2[i] = (i + 1) * d3[i + 1];
   for (int i = 0; i < 2; i++) d1[i] = (i + 1) * d2[i + 1];
-  double r1[1], r2[2], r3[3];
+  double r1[4] = {0, 0, 0, 0}, r2[4] = {0, 0, 0, 0}, r3[4] = {0, 0, 0, 0};
   int n1 = 0;
   if (!(fabs(d1[0]) > 1000 * fabs(d1[1]))) {
     r1[0] = -d1[0] / d1[1];
@@ -612,7 +626,7 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
     for (int i = 0; i < 4; i++) d3[i] = (i + 1) * poly[i + 1];
     for (int i = 0; i < 3; i++) d2[i] = (i + 1) * d3[i + 1];
     for (int i = 0; i < 2; i++) d1[i] = (i + 1) * d2[i + 1];
-    double r1[1], r2[2], r3[3];
+    double r1[4] = {0, 0, 0, 0}, r2[4] = {0, 0, 0, 0}, r3[4] = {0, 0, 0, 0};
     int n1 = 0;
     if (!(fabs(d1[0]) > 1000 * fabs(d1[1]))) {
       r1[0] = -d1[0] / d1[1];
@@ -642,9 +656,11 @@ __device__ bool fix_pose_ambiguities(const V3* v, const V3* p, const V3& t, cons
       }
     }
   } else {
-  double roots[4];
+  double roots[4] = {0, 0, 0, 0};
   const int n_roots = solve_quartic_approx<false>(poly, roots, sub);
-  for (int i = 0; i < n_roots; i++) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {  // (static slots: the roots stay in registers)
+    if (i >= n_roots) break;
     const double t1 = roots[i], t2 = t1 * t1, t3 = t1 * t2, t4 = t1 * t3, t5 = t1 * t4;
     if (a2 - 2 * a0 + (3 * a3 - 6 * a1) * t1 + (6 * a4 - 8 * a2 + 10 * a0) * t2 + (-8 * a3 + 6 * a1) * t3 +
             (-6 * a4 + 3 * a2) * t4 + a3 * t5 >= 0) {
