@@ -81,6 +81,18 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// Number of set bits of `mask` below this lane.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// a wave's LDS stores visible to its other lanes (a wave-level barrier, no s_barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // value of lane + 1 (lane 63: 0): DPP wave_shl:1
 __device__ __forceinline__ uint32_t wave_read_next(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
@@ -370,6 +382,12 @@ __device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
 // ancestor with a smaller id, so the atomicMin never loses a link)
 #ifndef AT_CCL_LEAN_SYNC
 #define AT_CCL_LEAN_SYNC 1
+#endif
+#ifndef AT_CCL_UNION_LIST
+#define AT_CCL_UNION_LIST 1
+#endif
+#ifndef AT_CCL_HEAD_FIND
+#define AT_CCL_HEAD_FIND 1
 #endif
 __device__ __forceinline__ uint32_t lds_find(uint32_t* par, uint32_t n) {
   uint32_t p = lds_load(par + n);
@@ -683,6 +701,10 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
   __syncthreads();
   ph(3);
+#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
+  if (AT_THR_CUT == 1) return;
+#endif
+
   // write this tile's threshold plane (4 bytes per thread)
   {
     const int r = tid / (kCclTileW / 4), c4 = (tid % (kCclTileW / 4)) * 4;
@@ -707,10 +729,14 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   const uint8_t a = T(pr, pc), bb = T(pr, pc + 1), c = T(pr + 1, pc), d = T(pr + 1, pc + 1);
   const uint32_t F = slot_of<TWD>(bty, btx, 0), L = slot_of<TWD>(bty, btx, 1), R = slot_of<TWD>(bty, btx, 2);
   const uint32_t lane = lane_id();
+  bool headF, headL, headR;  // this block's F / L / R starts its run (the run's head)
   {
     const bool fg_left = btx > 0 && (a == 255 || c == 255) && (T(pr, pc - 1) == 255 || T(pr + 1, pc - 1) == 255);
     const bool bg_left = btx > 0 && ((a == 0 && T(pr, pc - 1) == 0) || (c == 0 && T(pr + 1, pc - 1) == 0));
     const bool bg_in = (a == 0 && bb == 0) || (c == 0 && d == 0);  // R(x) - L(x)
+    headF = !fg_left;
+    headL = !bg_left;
+    headR = !bg_in;
     const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
     const uint64_t lt = (1ull << lane) - 1;                          // lanes < this one
     const uint64_t fs = __ballot(!fg_left);  // run starts (btx == 0 always starts: rows never merge)
@@ -750,15 +776,82 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     if (!AT_CCL_LEAN_SYNC) __syncthreads();
   ph(5);
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
+#if AT_CCL_UNION_LIST
+    // the wave's unions (at most five per block, mostly none) compacted into a
+    // wave-private list in s_gid's storage (unused until the publish) and run with
+    // every lane busy: ceil(n / 64) union rounds instead of five divergent sites in a
+    // row, each as long as its slowest lane
+    constexpr int kUnionPairs = kCclTileNodes / (NT / 64) / 2;
+    uint32_t* wl = s_gid + (tid >> 6) * (2 * kUnionPairs);
+    uint32_t nq = 0;  // (uniform)
+    auto flush = [&]() {
+      wave_sync();  // the list's stores before the other lanes' reads
+      for (uint32_t i = lane; i < nq; i += 64) lds_union(s_par, wl[2 * i], wl[2 * i + 1]);
+      wave_sync();  // (the list may be refilled)
+      nq = 0;
+    };
+    auto push = [&](bool act, uint32_t a, uint32_t b) {
+      const uint64_t m = __ballot(act);
+      const uint32_t cnt = (uint32_t)__popcll(m);
+      if (nq + cnt > (uint32_t)kUnionPairs) flush();
+      if (act) {
+        const uint32_t pos = nq + lanes_below(m);
+        wl[2 * pos] = a;
+        wl[2 * pos + 1] = b;
+      }
+      nq += cnt;
+    };
+    push(tUL != kNone && !seen_fg(tUL), hF, tUL);
+    push(tU != kNone && tU != tUL && !seen_fg(tU), hF, tU);
+    push(tUR != kNone && tUR != tUL && tUR != tU && !seen_fg(tUR), hF, tUR);
+    push(tL != kNone && !(bg_left && tL == pR), hL, tL);
+    push(tR != kNone && !(bg_in && tR == tL), hR, tR);
+    if (nq) flush();
+#else
     if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
     if (tU != kNone && tU != tUL && !seen_fg(tU)) lds_union(s_par, hF, tU);
     if (tUR != kNone && tUR != tUL && tUR != tU && !seen_fg(tUR)) lds_union(s_par, hF, tUR);
     if (tL != kNone && !(bg_left && tL == pR)) lds_union(s_par, hL, tL);
     if (tR != kNone && !(bg_in && tR == tL)) lds_union(s_par, hR, tR);
+#endif
   }
 #undef T
   __syncthreads();
   ph(6);
+#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
+  if (AT_THR_CUT == 2) return;
+#endif
+
+#if AT_CCL_HEAD_FIND
+  // Every find path runs through run heads only (a run's other nodes point at its head,
+  // and unions and path halving only ever link heads), so only the heads are found --
+  // compacted per wave like the unions, with no barrier before the root writes (a root
+  // written over a head's word is its component's smallest slot, which a concurrent
+  // compression's atomicMin leaves, and a find that reads it lands on that root) --
+  // and every node's root is then its parent's word: two loads, no loop.
+  {
+    constexpr int kFindList = kCclTileNodes / (NT / 64);  // 3 per lane
+    uint32_t* wl = s_gid + (tid >> 6) * kFindList;       // (this wave's own slots of s_gid)
+    uint32_t nh = 0;                                      // (uniform)
+    auto push = [&](bool act, uint32_t v) {
+      const uint64_t m = __ballot(act);
+      if (act) wl[nh + lanes_below(m)] = v;
+      nh += (uint32_t)__popcll(m);
+    };
+    push(headF, F);
+    push(headL, L);
+    push(headR, R);
+    wave_sync();
+    for (uint32_t i = lane; i < nh; i += 64) {
+      const uint32_t h = wl[i];
+      s_par[h] = lds_find(s_par, h);
+    }
+    wave_sync();  // (a run's heads are in the lanes of its own wave: rows never straddle waves)
+  }
+  const uint32_t rF = s_par[s_par[F]], rL = s_par[s_par[L]], rR = s_par[s_par[R]];
+  ph(7);
+#else
+  (void)headF; (void)headL; (void)headR;
   const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
   // (no barrier before the root writes: each writes a node's final root -- the smallest
   // slot of its component, so a concurrent compression's atomicMin leaves it -- and a
@@ -768,6 +861,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   s_par[F] = rF;
   s_par[L] = rL;
   s_par[R] = rR;
+#endif
   // every slot's global node id, by its owner (the publish looks its roots' ids up
   // instead of decoding slot numbers: ~15 VALU per decode)
   const uint32_t idF = (uint32_t)(2 * (y0 / 2 + bty) * g.Wd + 2 * (x0 / 2 + btx)), idL = idF + g.Wd;
@@ -800,6 +894,10 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   count(rR, nbr);
   __syncthreads();
   ph(8);
+#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
+  if (AT_THR_CUT == 3) return;
+#endif
+
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
   const bool inimg = BY < g.BH && BX < g.BW;
@@ -1382,10 +1480,6 @@ __device__ uint32_t ht_slot_find(const uint64_t* keys, uint64_t key) {
 __device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v) {
   return (uint64_t)wave_shr1((uint32_t)v, 0) | ((uint64_t)wave_shr1((uint32_t)(v >> 32), 0) << 32);
 }
-// Number of set bits of `mask` below this lane.
-__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 
 // slot hash of a pair key in the tile's LDS table: the low word (the smaller label and
@@ -1641,15 +1735,21 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     if (lane == 0 && wtot) wbase = atomicAdd(&s_npts, wtot);
     wbase = __shfl(wbase, 0);
     uint32_t pos = wbase + below;
+    if (wbase + wtot <= (uint32_t)kBndStage) {  // (uniform) the usual step: every point staged
 #pragma unroll
-    for (int d = 0; d < 8; d++)
-      if ((hm >> d) & 1) {
-        const uint64_t k = make_qbp(rep[d >> 2], nb[d], xa + (d >> 2), y, d & 3, b2w[d >> 2]);
-        if (pos < (uint32_t)kBndStage) s_pts[pos] = k;
-        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = k;
-        else atomicOr(b.status + f, kStatusPointsOverflow);
-        pos++;
-      }
+      for (int d = 0; d < 8; d++)
+        if ((hm >> d) & 1) s_pts[pos++] = make_qbp(rep[d >> 2], nb[d], xa + (d >> 2), y, d & 3, b2w[d >> 2]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 8; d++)
+        if ((hm >> d) & 1) {
+          const uint64_t k = make_qbp(rep[d >> 2], nb[d], xa + (d >> 2), y, d & 3, b2w[d >> 2]);
+          if (pos < (uint32_t)kBndStage) s_pts[pos] = k;
+          else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = k;
+          else atomicOr(b.status + f, kStatusPointsOverflow);
+          pos++;
+        }
+    }
   }
 #else
   const int x = 1 + bi.x * 64 + threadIdx.x;
@@ -2586,6 +2686,11 @@ __device__ __forceinline__ double gm_interp(const GrayModel& g, double x, double
 
 // lexicographic 4-combinations of 10 maxima == Unrank (line_fit_filter.cu:709-728)
 __constant__ uint8_t c_combo[210][4] = {{0,1,2,3},{0,1,2,4},{0,1,2,5},{0,1,2,6},{0,1,2,7},{0,1,2,8},{0,1,2,9},{0,1,3,4},{0,1,3,5},{0,1,3,6},{0,1,3,7},{0,1,3,8},{0,1,3,9},{0,1,4,5},{0,1,4,6},{0,1,4,7},{0,1,4,8},{0,1,4,9},{0,1,5,6},{0,1,5,7},{0,1,5,8},{0,1,5,9},{0,1,6,7},{0,1,6,8},{0,1,6,9},{0,1,7,8},{0,1,7,9},{0,1,8,9},{0,2,3,4},{0,2,3,5},{0,2,3,6},{0,2,3,7},{0,2,3,8},{0,2,3,9},{0,2,4,5},{0,2,4,6},{0,2,4,7},{0,2,4,8},{0,2,4,9},{0,2,5,6},{0,2,5,7},{0,2,5,8},{0,2,5,9},{0,2,6,7},{0,2,6,8},{0,2,6,9},{0,2,7,8},{0,2,7,9},{0,2,8,9},{0,3,4,5},{0,3,4,6},{0,3,4,7},{0,3,4,8},{0,3,4,9},{0,3,5,6},{0,3,5,7},{0,3,5,8},{0,3,5,9},{0,3,6,7},{0,3,6,8},{0,3,6,9},{0,3,7,8},{0,3,7,9},{0,3,8,9},{0,4,5,6},{0,4,5,7},{0,4,5,8},{0,4,5,9},{0,4,6,7},{0,4,6,8},{0,4,6,9},{0,4,7,8},{0,4,7,9},{0,4,8,9},{0,5,6,7},{0,5,6,8},{0,5,6,9},{0,5,7,8},{0,5,7,9},{0,5,8,9},{0,6,7,8},{0,6,7,9},{0,6,8,9},{0,7,8,9},{1,2,3,4},{1,2,3,5},{1,2,3,6},{1,2,3,7},{1,2,3,8},{1,2,3,9},{1,2,4,5},{1,2,4,6},{1,2,4,7},{1,2,4,8},{1,2,4,9},{1,2,5,6},{1,2,5,7},{1,2,5,8},{1,2,5,9},{1,2,6,7},{1,2,6,8},{1,2,6,9},{1,2,7,8},{1,2,7,9},{1,2,8,9},{1,3,4,5},{1,3,4,6},{1,3,4,7},{1,3,4,8},{1,3,4,9},{1,3,5,6},{1,3,5,7},{1,3,5,8},{1,3,5,9},{1,3,6,7},{1,3,6,8},{1,3,6,9},{1,3,7,8},{1,3,7,9},{1,3,8,9},{1,4,5,6},{1,4,5,7},{1,4,5,8},{1,4,5,9},{1,4,6,7},{1,4,6,8},{1,4,6,9},{1,4,7,8},{1,4,7,9},{1,4,8,9},{1,5,6,7},{1,5,6,8},{1,5,6,9},{1,5,7,8},{1,5,7,9},{1,5,8,9},{1,6,7,8},{1,6,7,9},{1,6,8,9},{1,7,8,9},{2,3,4,5},{2,3,4,6},{2,3,4,7},{2,3,4,8},{2,3,4,9},{2,3,5,6},{2,3,5,7},{2,3,5,8},{2,3,5,9},{2,3,6,7},{2,3,6,8},{2,3,6,9},{2,3,7,8},{2,3,7,9},{2,3,8,9},{2,4,5,6},{2,4,5,7},{2,4,5,8},{2,4,5,9},{2,4,6,7},{2,4,6,8},{2,4,6,9},{2,4,7,8},{2,4,7,9},{2,4,8,9},{2,5,6,7},{2,5,6,8},{2,5,6,9},{2,5,7,8},{2,5,7,9},{2,5,8,9},{2,6,7,8},{2,6,7,9},{2,6,8,9},{2,7,8,9},{3,4,5,6},{3,4,5,7},{3,4,5,8},{3,4,5,9},{3,4,6,7},{3,4,6,8},{3,4,6,9},{3,4,7,8},{3,4,7,9},{3,4,8,9},{3,5,6,7},{3,5,6,8},{3,5,6,9},{3,5,7,8},{3,5,7,9},{3,5,8,9},{3,6,7,8},{3,6,7,9},{3,6,8,9},{3,7,8,9},{4,5,6,7},{4,5,6,8},{4,5,6,9},{4,5,7,8},{4,5,7,9},{4,5,8,9},{4,6,7,8},{4,6,7,9},{4,6,8,9},{4,7,8,9},{5,6,7,8},{5,6,7,9},{5,6,8,9},{5,7,8,9},{6,7,8,9}};
+
+// the combinations in colexicographic order (by m3, then m2, m1, m0), as indices into
+// c_combo: those with m3 < cnt are exactly the first C(cnt, 4), so a blob's FitQuads
+// loop visits only its valid combinations
+__constant__ uint8_t c_colex[210] = {0,1,7,28,84,2,8,29,85,13,34,90,49,105,140,3,9,30,86,14,35,91,50,106,141,18,39,95,54,110,145,64,120,155,175,4,10,31,87,15,36,92,51,107,142,19,40,96,55,111,146,65,121,156,176,22,43,99,58,114,149,68,124,159,179,74,130,165,185,195,5,11,32,88,16,37,93,52,108,143,20,41,97,56,112,147,66,122,157,177,23,44,100,59,115,150,69,125,160,180,75,131,166,186,196,25,46,102,61,117,152,71,127,162,182,77,133,168,188,198,80,136,171,191,201,205,6,12,33,89,17,38,94,53,109,144,21,42,98,57,113,148,67,123,158,178,24,45,101,60,116,151,70,126,161,181,76,132,167,187,197,26,47,103,62,118,153,72,128,163,183,78,134,169,189,199,81,137,172,192,202,206,27,48,104,63,119,154,73,129,164,184,79,135,170,190,200,82,138,173,193,203,207,83,139,174,194,204,208,209};
 
 struct LineFitOut {
   double err, mse;
@@ -3691,9 +3796,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   // over the key area (its compact words were last read by the prefix lookups)
   SegFits& seg = *reinterpret_cast<SegFits*>(S.keys);
   static_assert(sizeof(SegFits) <= sizeof(S.keys), "segment fits must fit over the keys");
-  for (int ci = tid; cnt >= 4 && ci < kNMaxima * kNMaxima; ci += NT) {
-    const int a = ci / kNMaxima, bb = ci % kNMaxima;
-    if (a != bb && a < cnt && bb < cnt) {
+  // the cn x cn (segment start, end) pairs of the top cn = min(cnt, 10) peaks, one per
+  // lane (cn <= 8: one round)
+  const int cn = min(cnt, kNMaxima);
+  const float rcn = 1.0f / (float)max(cn, 1);
+  for (int ci = tid; cnt >= 4 && ci < cn * cn; ci += NT) {
+    const int a = (int)(((float)ci + 0.5f) * rcn), bb = ci - a * cn;  // (exact: ci + 0.5 is >= 0.05 from a multiple of cn)
+    if (a != bb) {
       const LineFitOut o = fit_line_v<false, true>(seg_moments(a, bb));
       seg.err[a][bb] = o.err;
       seg.mse[a][bb] = o.mse;
@@ -3704,16 +3813,19 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   team_sync<NT>();
   phase(7);
   if (AT_DIAG_STOP(prm, 7)) return;
-  // 210 lexicographic combinations; each lane keeps its first minimum
+  // the C(cnt, 4) valid combinations (the first in colexicographic order); each lane
+  // keeps its minimum, the lowest lexicographic index on ties (the reference's first)
   double err = DBL_MAX;
   uint32_t bt = 0xffffffffu;
   const double mse_max = (double)prm.max_line_fit_mse;
-  for (int ci = tid; ci < 210; ci += NT) {
+  const int ncomb = cnt < 4 ? 0 : cnt >= kNMaxima ? 210 : (cnt * (cnt - 1) * (cnt - 2) * (cnt - 3)) / 24;
+  for (int cj = tid; cj < ncomb; cj += NT) {
     double e4 = DBL_MAX;
-    if (cnt >= 4) {
+    const int ci = (int)combo[210 + cj];
+    {
       const uint32_t cb = combo[ci];  // LDS copy of c_combo: no vector-memory wait in this loop
       const int m0 = cb & 0xff, m1 = (cb >> 8) & 0xff, m2 = (cb >> 16) & 0xff, m3 = cb >> 24;
-      if (m3 < cnt && !(seg.mse[m0][m1] > mse_max)) {
+      if (!(seg.mse[m0][m1] > mse_max)) {
         if (!(seg.mse[m1][m2] > mse_max)) {
           const double dot =
               seg.p[m0][m1][0] * seg.p[m1][m2][0] + seg.p[m0][m1][1] * seg.p[m1][m2][1];
@@ -3724,7 +3836,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
         }
       }
     }
-    if (bt == 0xffffffffu || e4 < err) { err = e4; bt = (uint32_t)ci; }
+    if (bt == 0xffffffffu || e4 < err || (e4 == err && (uint32_t)ci < bt)) { err = e4; bt = (uint32_t)ci; }
   }
   // BlockReduce(MinQuadError): minimum error, first (lowest) combination on ties
 #pragma unroll
@@ -3859,10 +3971,15 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   team_sync<NT>();
 }
 
+// s_combo[0, 210): the combinations packed (m0 | m1 << 8 | m2 << 16 | m3 << 24) in
+// c_combo's lexicographic order (the reference's tie-break order); s_combo[210, 420):
+// c_colex, the lexicographic indices in colexicographic order
 __device__ __forceinline__ void load_combos(uint32_t* s_combo, int tid, int nt) {
-  for (int i = tid; i < 210; i += nt)
+  for (int i = tid; i < 210; i += nt) {
     s_combo[i] = (uint32_t)c_combo[i][0] | ((uint32_t)c_combo[i][1] << 8) | ((uint32_t)c_combo[i][2] << 16) |
                  ((uint32_t)c_combo[i][3] << 24);
+    s_combo[210 + i] = c_colex[i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -4176,7 +4293,7 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
     kt_slot = atomicAdd(b.kgrid, 1u);
     if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
   }
-  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  __shared__ uint32_t s_combo[420], s_cnt[kNumCls];
   load_combos(s_combo, tid, NT);
   if (tid < kNumCls) s_cnt[tid] = min(b.ncls[tid], b.wcap);
   large_blob_loop<NT, CAP, FUSE>(b, g, prm, S, s_combo, s_cnt, nlo, blockIdx.x, c0, c1, launch);
@@ -4207,7 +4324,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
     kt_slot = atomicAdd(b.kgrid, 1u);
     if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
   }
-  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  __shared__ uint32_t s_combo[420], s_cnt[kNumCls];
   load_combos(s_combo, threadIdx.x, 256);
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
   __syncthreads();
@@ -4229,7 +4346,7 @@ __global__ __launch_bounds__(512) void k_blob_lat(DevBufs b, Geom g, Params prm)
   using SS = BlobShared<64, kSmallBlob>;
   static_assert(8 * sizeof(SS) <= sizeof(SL), "eight small-blob waves fit in a large team's LDS");
   __shared__ __attribute__((aligned(16))) unsigned char s_raw[sizeof(SL)];
-  __shared__ uint32_t s_combo[210], s_cnt[kNumCls];
+  __shared__ uint32_t s_combo[420], s_cnt[kNumCls];
   const int tid = threadIdx.x;
   kt_begin(b, 9);
   load_combos(s_combo, tid, 512);
