@@ -910,8 +910,14 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   // the tile's local roots of components reaching its border (with pixels), listed for
   // the cross-tile merge (k_ccl_merge in throughput mode, k_ccl_border + k_ccl_roots in latency mode)
   const bool lF = cF && (wF & kTouchBit), lL = cL && (wL & kTouchBit), lR = cR && (wR & kTouchBit);
-  const uint32_t iF = lF ? atomicAdd(&s_nlr, 1u) : 0u, iL = lL ? atomicAdd(&s_nlr, 1u) : 0u,
-                 iR = lR ? atomicAdd(&s_nlr, 1u) : 0u;
+  // (their list slots: one LDS atomic per wave -- the same-address atomics of a wave's
+  // listed roots serialized, three times over)
+  const uint64_t mlF = __ballot(lF), mlL = __ballot(lL), mlR = __ballot(lR);
+  const uint32_t nlF = (uint32_t)__popcll(mlF), nlL = (uint32_t)__popcll(mlL), nlR = (uint32_t)__popcll(mlR);
+  uint32_t lb0 = 0;
+  if (lane == 0 && nlF + nlL + nlR) lb0 = atomicAdd(&s_nlr, nlF + nlL + nlR);
+  lb0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lb0);
+  const uint32_t iF = lb0 + lanes_below(mlF), iL = lb0 + nlF + lanes_below(mlL), iR = lb0 + nlF + nlL + lanes_below(mlR);
   constexpr bool kKeep = TWD != 32;
   if constexpr (kKeep) {  // list slots of the roots, for the border descriptor
     if (lF) s_li[F] = (uint16_t)iF;
@@ -1558,6 +1564,9 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 #ifndef AT_BND_TWO
 #define AT_BND_TWO 1
 #endif
+#ifndef AT_BND_FLAT
+#define AT_BND_FLAT 1
+#endif
 // KEPT (throughput mode): the size test comes with the root word (k_ccl_merge);
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
@@ -1667,6 +1676,25 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
 #pragma unroll
       for (int d = 0; d < 4; d++) nb[4 * j + d] = 0;
       const uint32_t v0 = (ra >> (8 * j + 8)) & 0xff;
+#if AT_BND_FLAT
+      // branch-free: the five labels read whatever the pixel (the halo holds every
+      // address; a label is used only where its direction's bit is set), so no exec-mask
+      // region per direction
+      const uint32_t vl = (ra >> (8 * j)) & 0xff, vr = (ra >> (8 * j + 16)) & 0xff;
+      const uint32_t vdl = (rb >> (8 * j)) & 0xff, vd = (rb >> (8 * j + 8)) & 0xff, vdr = (rb >> (8 * j + 16)) & 0xff;
+      const int e0 = eb + j + 1, ed = e0 + kTC;
+      const bool pv = xa + j <= g.Wd - 2 && y <= g.Hd - 2 && v0 != 127;
+      rep[j] = s_tlab[e0];
+      b2w[j] = v0 == 0;
+      nb[4 * j] = s_tlab[e0 + 1];
+      nb[4 * j + 1] = s_tlab[ed + 1];
+      nb[4 * j + 2] = s_tlab[ed];
+      nb[4 * j + 3] = s_tlab[ed - 1];
+      const bool dedup = vl != 127 && vd != 127 && vd != vl && xa + j != 1;
+      const uint32_t pm = (v0 + vr == 255 ? 1u : 0u) | (v0 + vdr == 255 ? 2u : 0u) | (v0 + vd == 255 ? 4u : 0u) |
+                          (!dedup && v0 + vdl == 255 ? 8u : 0u);
+      hm |= pv ? pm << (4 * j) : 0u;
+#else
       if (xa + j <= g.Wd - 2 && y <= g.Hd - 2 && v0 != 127) {
         const uint32_t vl = (ra >> (8 * j)) & 0xff, vr = (ra >> (8 * j + 16)) & 0xff;
         const uint32_t vdl = (rb >> (8 * j)) & 0xff, vd = (rb >> (8 * j + 8)) & 0xff, vdr = (rb >> (8 * j + 16)) & 0xff;
@@ -1679,6 +1707,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
         const bool dedup = vl != 127 && vd != 127 && vd != vl && xa + j != 1;
         if (!dedup && v0 + vdl == 255) { hm |= 8u << (4 * j); nb[4 * j + 3] = s_tlab[ed - 1]; }
       }
+#endif
     }
     // pair histogram: the lane's first pair with the count of its points in it (labels
     // are < 2^20 -- decimated planes of at most 1024 x 1024 -- so label equality is
