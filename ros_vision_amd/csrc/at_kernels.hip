@@ -743,14 +743,11 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     const int hf = 63 - __builtin_clzll(fs & le);
     const uint32_t hF = F - (uint32_t)(lane - hf);
     const uint64_t sl = __ballot(!bg_left), sr = __ballot(!bg_in);
-    uint32_t hL, hR;
-    if (!bg_left) {
-      hL = L;
-    } else {  // last run start before L(x): in the nearest lane below with a start, its R if R starts there
-      const int hl = 63 - __builtin_clzll((sl | sr) & lt);
-      hL = ((sr >> hl) & 1) ? slot_of<TWD>(bty, btx - (lane - hl), 2) : slot_of<TWD>(bty, btx - (lane - hl), 1);
-    }
-    hR = bg_in ? hL : R;
+    // L's run head: L itself, or the last run start before L(x) -- in the nearest lane
+    // below with a start, its R if R starts there (selects, no branch)
+    const int hl = 63 - __builtin_clzll(((sl | sr) & lt) | 1ull);
+    const uint32_t hLl = ((sr >> hl) & 1) ? slot_of<TWD>(bty, btx - (lane - hl), 2) : slot_of<TWD>(bty, btx - (lane - hl), 1);
+    const uint32_t hL = bg_left ? hLl : L, hR = bg_in ? hL : R;
     s_par[F] = hF;
     s_par[L] = hL;
     s_par[R] = hR;
@@ -758,15 +755,19 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   ph(4);
     // heads of the run(s) above this block's vertical links (read before any union)
     constexpr uint32_t kNone = 0xffffffffu;
-    uint32_t tUL = kNone, tU = kNone, tUR = kNone, tL = kNone, tR = kNone;
-    if (bty > 0) {
-      if (btx > 0 && a == 255 && T(pr - 1, pc - 1) == 255) tUL = s_par[slot_of<TWD>(bty - 1, btx - 1, 0)];
-      if ((a == 255 || bb == 255) && (T(pr - 1, pc) == 255 || T(pr - 1, pc + 1) == 255))
-        tU = s_par[slot_of<TWD>(bty - 1, btx, 0)];
-      if (btx < kCclBW - 1 && bb == 255 && T(pr - 1, pc + 2) == 255) tUR = s_par[slot_of<TWD>(bty - 1, btx + 1, 0)];
-      if (a == 0 && T(pr - 1, pc) == 0) tL = s_par[slot_of<TWD>(bty - 1, btx, 1)];
-      if (bb == 0 && T(pr - 1, pc + 1) == 0) tR = s_par[slot_of<TWD>(bty - 1, btx, 2)];
-    }
+    // (branch-free: the five words read whatever the block -- block row 0 reads its own
+    // row and the halo row of s_t, both in bounds -- and kept where the link holds)
+    const int uy = bty > 0 ? bty - 1 : 0, ulx = btx > 0 ? btx - 1 : 0, urx = btx < kCclBW - 1 ? btx + 1 : btx;
+    const uint32_t vUL = s_par[slot_of<TWD>(uy, ulx, 0)], vU = s_par[slot_of<TWD>(uy, btx, 0)],
+                   vUR = s_par[slot_of<TWD>(uy, urx, 0)], vL = s_par[slot_of<TWD>(uy, btx, 1)],
+                   vR = s_par[slot_of<TWD>(uy, btx, 2)];
+    const uint8_t u0 = T(pr - 1, pc - 1), u1 = T(pr - 1, pc), u2 = T(pr - 1, pc + 1), u3 = T(pr - 1, pc + 2);
+    const bool up = bty > 0;
+    const uint32_t tUL = up && btx > 0 && a == 255 && u0 == 255 ? vUL : kNone;
+    const uint32_t tU = up && (a == 255 || bb == 255) && (u1 == 255 || u2 == 255) ? vU : kNone;
+    const uint32_t tUR = up && btx < kCclBW - 1 && bb == 255 && u3 == 255 ? vUR : kNone;
+    const uint32_t tL = up && a == 0 && u1 == 0 ? vL : kNone;
+    const uint32_t tR = up && bb == 0 && u2 == 0 ? vR : kNone;
     // the left neighbour's targets (same wave: rows never straddle waves)
     const uint32_t pUL = __shfl_up(tUL, 1), pU = __shfl_up(tU, 1), pUR = __shfl_up(tUR, 1), pR = __shfl_up(tR, 1);
     // (no barrier before the unions: a target read while another block's union or path
