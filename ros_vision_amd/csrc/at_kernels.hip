@@ -1181,6 +1181,10 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
 // workgroup in global memory (k_ccl_border's unions, k_ccl_roots' pass, the kept
 // bits; ccl_ovf set).
 // ---------------------------------------------------------------------------
+#ifndef AT_MERGE_UNION_LIST
+#define AT_MERGE_UNION_LIST 1
+#endif
+constexpr int kMergeList = 64;  // link pairs per wave list (k_ccl_merge)
 constexpr int kMergePer = (kMergeCapMax + 1023) / 1024;  // listed roots per thread
 constexpr int kMergeItems = 2;                          // border blocks per thread per pass
 
@@ -1351,6 +1355,22 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     return (uint32_t)reinterpret_cast<const uint16_t*>(desc + (size_t)t * CclDesc::kWords + w)[i];
   };
   const int n0 = ntl * kBW, n1 = n0 + ntl * kBH, nitems = n1 + ntl * (kBH - 1);
+#if AT_MERGE_UNION_LIST
+  // a wave's links (ten candidate sites per lane per pass) compacted by ballot into a
+  // wave-private list and run with every lane busy, as in k_thr_ccl -- in the dynamic
+  // LDS past the roots when it has room (the usual frame), else the sites directly
+  const size_t lused = ((((size_t)total * 10 + 3) & ~(size_t)3) + (cnt_lds ? (size_t)total * 4 : 0) + 7) & ~(size_t)7;
+  const bool ulist = fits && lused + (size_t)16 * kMergeList * 8 <= (size_t)g.merge_lds;  // (uniform)
+  uint32_t* wl = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_key) + lused) + (tid >> 6) * (2 * kMergeList);
+  const uint32_t wlane = lane_id();
+  uint32_t nl = 0;  // (uniform per wave)
+  auto lflush = [&]() {
+    wave_sync();
+    for (uint32_t i = wlane; i < nl; i += 64) merge_union(s_key, wl[2 * i], wl[2 * i + 1]);
+    wave_sync();
+    nl = 0;
+  };
+#endif
   for (int j0 = 0; j0 < nitems; j0 += 1024 * kMergeItems) {
     uint32_t su[kMergeItems][5], sv[kMergeItems][5];  // slot pair per link (0xffffffff: none)
 #pragma unroll
@@ -1415,9 +1435,27 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
         const bool on = su[q][k] != 0xffffffffu && sv[q][k] < (uint32_t)total && su[q][k] < (uint32_t)total;
         const uint32_t pair = on ? (su[q][k] << 16 | sv[q][k]) : 0xffffffffu;
         const uint32_t prev = wave_shr1(pair, 0xfffffffeu);
+#if AT_MERGE_UNION_LIST
+        if (ulist) {
+          const bool act = on && pair != prev;
+          const uint64_t m = __ballot(act);
+          const uint32_t c = (uint32_t)__popcll(m);
+          if (nl + c > (uint32_t)kMergeList) lflush();
+          if (act) {
+            const uint32_t pos = nl + lanes_below(m);
+            wl[2 * pos] = su[q][k];
+            wl[2 * pos + 1] = sv[q][k];
+          }
+          nl += c;
+          continue;
+        }
+#endif
         if (on && pair != prev) merge_union(s_key, su[q][k], sv[q][k]);
       }
   }
+#if AT_MERGE_UNION_LIST
+  if (ulist && nl) lflush();
+#endif
   __syncthreads();
   stamp(3);
   // (3) component sizes at the roots: in LDS, or (counts not in LDS) every listed non-root
