@@ -93,6 +93,9 @@ def parse(argv=None):
                     help="local: every rank renders its own frames into its HBM (weak scaling, no data-path "
                          "collective); scatter: frames live on rank 0 and are scattered each step over RCCL "
                          "(north-star topology), detection records gathered back to rank 0")
+    ap.add_argument("--scatter-leg-steps", type=int, default=None,
+                    help="N > 1 with --ingest local: steps of the scatter leg run after the timed region (the "
+                         "north-star topology, reported as scatter_leg; default = --steps; 0 = skip)")
     return ap.parse_args(argv)
 
 
@@ -319,37 +322,39 @@ def main():
     base = d_frames.data_ptr()
     npool = args.pool * copies
     assert npool >= B, "the frames resident per GPU (--pool x --hbm-copies) must hold one batch"
-    dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank, pinned_out=scatter) for _ in range(args.instances)]
-    ingest = None
-    if scatter:
-        # rank 0 holds every rank's frame pool in its HBM; each step scatters B frames per rank
+    # (peers of a scatter run, or of the N > 1 line's scatter leg, send their records
+    # from a page-locked output buffer)
+    dets = [rva.GpuDetector(W, H, max_batch=B, device=local_rank, pinned_out=scatter or world > 1)
+            for _ in range(args.instances)]
+    rec_cap = 32  # detection records per frame in the fixed-size message; more follow in the overflow one
+    rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)
+    topo = {}    # the scatter topology's ingest / gather (set up on first use)
+
+    def setup_scatter():
+        """rank 0 holds every rank's frame pool in its HBM; each step sends B frames to
+        every peer (multigpu.ScatterIngest), records return by multigpu.RecordGather"""
+        if topo:
+            return topo["ingest"], topo["gather"]
         root_pool = None
+        mine = torch.from_numpy(frames).to("cuda")
+        # every rank's rendered pool to rank 0 (set-up, untimed: one send per peer instead
+        # of rank 0 rendering them all)
         if rank == 0:
             root_pool = torch.empty((world, npool) + frames.shape[1:], dtype=torch.uint8, device="cuda")
-            for r in range(world):
-                root_pool[r] = torch.from_numpy(render_pool(args, r) if r else frames).repeat(copies, 1, 1)
-        ingest = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
-        rec_cap = 32  # detection records per frame in the fixed-size message; more follow in the overflow one
-        rec_bytes = rec_cap * ctypes.sizeof(rva.detector.AtDetection)
-        copied = {}  # detector -> event after the async copy out of its pinned buffer
-        gather = multigpu.RecordGather(dist, B, rec_bytes, "cuda")
-
-    def gather_results(d, s):
-        """Every detection record of the other ranks' batches -> rank 0
-        (multigpu.RecordGather: RCCL point-to-point): a fixed-size row of the first
-        rec_cap records per frame with the frame's true count, read from the pinned
-        buffer at_collect wrote by an async copy, plus an overflow message with the
-        records past rec_cap of the frames that have more.  Rank 0's own stay in its
-        host buffer; at world size 1 nothing moves."""
-        if world == 1:
-            return
-        if rank == 0:
-            gather.post(s)
+            root_pool[0] = mine.repeat(copies, 1, 1)
+            for r in range(1, world):
+                dist.recv(mine, src=r)
+                root_pool[r] = mine.repeat(copies, 1, 1)
         else:
-            counts = [d._n[f] for f in range(B)]
-            gather.post(s, d._out_t.view(B, -1)[:, :rec_bytes], torch.tensor(counts, dtype=torch.int32),
-                        multigpu.overflow_from(counts, rec_cap, d.frame_record_bytes))
-            copied[id(d)] = gather.copied[s % 2]
+            dist.send(mine, dst=0)
+        del mine
+        topo["ingest"] = multigpu.ScatterIngest(dist, root_pool, B, frames.shape[1:], "cuda", nbuf=args.instances)
+        topo["gather"] = multigpu.RecordGather(dist, B, rec_bytes, "cuda")
+        return topo["ingest"], topo["gather"]
+
+    ingest = gather = None
+    if scatter:
+        ingest, gather = setup_scatter()
 
     runner = StreamRunner(dets, base, stride, npool, B)
 
@@ -364,37 +369,11 @@ def main():
         return runner.run(nsteps, step0)
 
     def run_scatter(nsteps, step0):
-        """The scatter of step k+1 overlaps the detection of steps k-instances+2 .. k:
-        the same in-flight depth as the local-ingest loop (one frame buffer per
-        instance; a buffer is rescattered only after the batch that read it is
-        collected)."""
-        ndet = 0
-        ni = len(dets)
-        inflight = []
-
-        def drain():
-            pd, ps = inflight.pop(0)
-            if id(pd) in copied:  # its pinned buffer may still be copied from
-                copied[id(pd)].synchronize()
-            n = sum(pd.collect(counts_only=True))
-            gather_results(pd, ps)
-            return n
-
-        ingest.start(step0)
-        for s in range(step0, step0 + nsteps):
-            d = dets[(s - step0) % ni]
-            buf = ingest.ready(s, detector=d)  # stream dependency, no host wait
-            d.enqueue_device(buf.data_ptr(), stride, B)
-            inflight.append((d, s))
-            if len(inflight) == ni:
-                ndet += drain()
-            if s + 1 < step0 + nsteps:
-                ingest.start(s + 1)  # its buffer was read by step s+1-instances, collected above
-        while inflight:
-            ndet += drain()
-        gather.drain()
-        ingest.drain()
-        return ndet
+        """multigpu.ScatterLoop: frames from rank 0, records back to rank 0."""
+        ingest, gather = setup_scatter()
+        if "loop" not in topo:
+            topo["loop"] = multigpu.ScatterLoop(dist, dets, ingest, gather, B, stride, rec_cap)
+        return topo["loop"].run(nsteps, step0)
 
     if args.isolated_only:  # (the rocprofv3 command of profiles/: every launch serialized)
         iso = isolated_kernel_times(dets[0], batch_ptr, stride, B, max(1, args.isolated_batches))
@@ -467,6 +446,27 @@ def main():
         ndet = int(nd.item())
     total_frames = world * args.steps * B
     fps = total_frames / elapsed
+
+    # N > 1 with local ingest: the north-star topology beside the headline, so a 1->8
+    # run measures it too -- frames from rank 0 over RCCL, records back to rank 0
+    scatter_leg = None
+    leg_steps = args.steps if args.scatter_leg_steps is None else args.scatter_leg_steps
+    if world > 1 and not scatter and leg_steps > 0:
+        _, leg_gather = setup_scatter()
+        run_scatter(len(dets), 0)  # warm-up: buffers, the gather's communicator
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        recv0 = leg_gather.records_received
+        nd_leg = run_scatter(leg_steps, step0=len(dets))
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        leg_el = time.perf_counter() - t1
+        at_root = nd_leg + leg_gather.records_received - recv0 if rank == 0 else None
+        leg_el, leg_det = multigpu.reduce_max_sum(dist, leg_el, nd_leg, "cuda")
+        scatter_leg = multigpu.scatter_leg_summary(world, leg_steps, B, stride, leg_el, leg_det, at_root)
 
     # every kernel on its own (one batch in flight): the headline roofline kernel is
     # the one with the longest isolated launch
@@ -628,6 +628,7 @@ def main():
         "host_ingest": host_ingest,
         "detections_per_frame": round(ndet / total_frames, 3),
         "records_at_rank0": records_at_root,
+        "scatter_leg": scatter_leg,
         "roofline": roofline,
         "roofline_concurrent": roofline_concurrent,
         "roofline_pipeline": {"bound": "hbm", "achieved": round(per_gpu_fps * pipe_bytes / 1e9, 3),

@@ -4560,6 +4560,9 @@ __device__ void decode_finish(const DevBufs& b, int lane, uint32_t nq) {
 // one per CU -- 64 left the 1080p stage at 4.03 ms per 192 frames serialized, 1.69 ms at 256
 // (concurrent 1080p throughput +1.5 %, profiles/r04y)
 #endif
+#ifndef AT_BIG_NT
+#define AT_BIG_NT 512  // threads per team of the CAP-8192 launch (16 keys per thread: register theta sort)
+#endif
 #ifndef AT_FORK_SMALL
 #define AT_FORK_SMALL 1  // latency mode: fork the small-blob kernel (0: the large-blob one)
 #endif
@@ -5420,20 +5423,23 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     } else if (B < kWideBlobMaxBatch || prm.wide_blob) {  // (latency: one launch, longest blob first)
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
-    } else if (cap4k && AT_MID_BLOB) {
-      // throughput: blobs of 1025-4096 points in 256-thread teams, the 513-1024-point
-      // class (two thirds of the large blobs at 720p) in 128-thread teams (CAP 1024:
-      // the same 8 points per thread as the one-wave kernel; barriers over two waves)
-      if (AT_MID_BLOB >= 2) {  // (experiment: 1025-2048 points in their own launch too)
-        hipLaunchKernelGGL((k_blob<256, 4096>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, 1, 0);
-        hipLaunchKernelGGL((k_blob<AT_MID2_NT, 2048>), dim3(nblobwg * 256 / AT_MID2_NT), dim3(AT_MID2_NT), 0, s, b, g, prm, 0u, 1, 2, 2);
-      } else {
-        hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, 2, 0);
-      }
-      hipLaunchKernelGGL((k_blob<128, 1024>), dim3(2 * nblobwg), dim3(128), 0, s, b, g, prm, 0u, 2, 3, 1);
+    } else if (AT_MID_BLOB) {
+      // throughput: blobs of 1025-4096 points (size classes 0 .. nlarge-2) in 256-thread
+      // teams, the 513-1024-point class (nlarge-1: two thirds of the large blobs) in
+      // 128-thread teams (CAP 1024: the same 8 points per thread as the one-wave kernel;
+      // barriers over two waves); geometries whose blobs exceed 4096 points (1080p) add a
+      // launch of CAP-8192 teams over those (class 0 above 4096), AT_BIG_NT threads each:
+      // 16 keys per thread keep its theta sort in registers (256-thread teams held 32 and
+      // fell back to a bitonic sort of 8192 keys)
+      const int lo = prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg;
+      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(lo), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge - 1, 0);
+      hipLaunchKernelGGL((k_blob<128, 1024>), dim3(2 * nblobwg), dim3(128), 0, s, b, g, prm, 0u, g.nlarge - 1, g.nlarge, 1);
+      if (!cap4k)
+        hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g,
+                           prm, 4096u, 0, 1, 2);
     } else {
       hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
-      if (!cap4k) hipLaunchKernelGGL((k_blob<256, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(256), 0, s, b, g, prm, 4096u, 0, 1, 1);
+      if (!cap4k) hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g, prm, 4096u, 0, 1, 1);
     }
     tk(9, s, 1);
   };

@@ -220,20 +220,38 @@ class RecordGather:
     Message order per peer (point-to-point order is the matching order): header(s),
     overflow(s) if any, header(s + 1) ...  Rank 0 learns the size of overflow(s) from
     header(s), so before posting header(s + 1) it waits for header(s) (one step behind
-    the detector) and posts the overflow receive first."""
+    the detector) and posts the overflow receive first.
 
-    def __init__(self, dist, batch: int, rec_bytes: int, device):
+    The gather runs in a process group of its own (``dist.new_group``, created
+    collectively by every rank in the constructor): with backend "nccl" that is an RCCL
+    communicator, and so a stream, separate from ScatterIngest's.  On one shared
+    communicator a peer's queue [header(s)][overflow(s)][receive frames(s + n)] and rank
+    0's [receive header(s)][send frames(s + n)][receive overflow(s)] each wait on a
+    transfer the other side queued behind its own, which only progresses while RCCL can
+    buffer the overflow (a dense frame's overflow exceeds that).  Rank 0 reads the
+    headers' counts on a side stream (copy to page-locked memory, event), not by
+    synchronizing torch's current stream."""
+
+    def __init__(self, dist, batch: int, rec_bytes: int, device, group=None):
         import torch
         self.dist, self.world, self.rank = dist, dist.get_world_size(), dist.get_rank()
         self.device = device
         self.cuda = str(device).startswith("cuda")
+        # the gather's own communicator (every rank constructs RecordGather, so the
+        # collective new_group call matches on all of them)
+        self.group = group if group is not None else (dist.new_group(list(range(self.world)))
+                                                      if self.world > 1 else None)
+        self.side = torch.cuda.Stream(device) if (self.cuda and self.world > 1) else None
         self.batch, self.rec_bytes = batch, rec_bytes
         self.cap = rec_bytes // _rec_size()
         row = rec_bytes + 4
         self.send = [torch.empty((batch, row), dtype=torch.uint8, device=device) for _ in range(2)]
         self.cnt = [torch.empty((batch,), dtype=torch.int32) for _ in range(2)]
+        # rank 0: the peers' counts of a header, read back to the host
+        self.hcnt = torch.empty((max(1, self.world - 1), batch), dtype=torch.int32)
         if self.cuda:
             self.cnt = [c.pin_memory() for c in self.cnt]
+            self.hcnt = self.hcnt.pin_memory()
         self.recv = ([{r: torch.empty((batch, row), dtype=torch.uint8, device=device) for r in range(1, self.world)}
                       for _ in range(2)] if self.rank == 0 else None)
         self.ovf = [None, None]      # peer: overflow send buffer; rank 0: {peer: receive buffer}
@@ -248,23 +266,38 @@ class RecordGather:
             w.wait()
         self.work[i] = self.owork[i] = None
 
+    def _p2p(self, op, tensor, peer):
+        return self.dist.P2POp(op, tensor, peer, group=self.group)
+
     def _resolve(self, step):
         """Rank 0: header(step) has to have arrived; post its overflow receives."""
         import torch
         i = step % 2
-        for w in (self.work[i] or []):
-            w.wait()
-        self.work[i] = None
         if self.cuda:
-            torch.cuda.current_stream().synchronize()  # the headers are in HBM: read their counts
+            # the headers are in HBM: a side stream waits for their arrival and copies the
+            # count columns to page-locked memory; the host waits for that copy only
+            with torch.cuda.stream(self.side):
+                for w in (self.work[i] or []):
+                    w.wait()
+                for r in range(1, self.world):
+                    self.hcnt[r - 1].view(torch.uint8).view(-1, 4).copy_(self.recv[i][r][:, :4], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            ev.synchronize()
+        else:
+            for w in (self.work[i] or []):
+                w.wait()
+            for r in range(1, self.world):
+                self.hcnt[r - 1].copy_(self.recv[i][r][:, :4].contiguous().view(torch.int32).ravel())
+        self.work[i] = None
         ovf, ops = {}, []
         for r in range(1, self.world):
-            counts = self.recv[i][r][:, :4].contiguous().view(torch.int32).ravel().cpu().numpy()
+            counts = self.hcnt[r - 1].numpy().copy()
             self.records_received += int(counts.sum())
             m = overflow_bytes(counts, self.cap)
             if m:
                 ovf[r] = torch.empty((m,), dtype=torch.uint8, device=self.device)
-                ops.append(self.dist.P2POp(self.dist.irecv, ovf[r], r))
+                ops.append(self._p2p(self.dist.irecv, ovf[r], r))
         self.ovf[i] = ovf
         self.owork[i] = self.dist.batch_isend_irecv(ops) if ops else None
 
@@ -277,7 +310,7 @@ class RecordGather:
             while self.unresolved:  # overflow(s) precedes header(s + 1) on every link
                 self._resolve(self.unresolved.pop(0))
             self._wait(i)  # the buffer's previous transfer (step - 2)
-            self.work[i] = d.batch_isend_irecv([d.P2POp(d.irecv, self.recv[i][r], r) for r in range(1, self.world)])
+            self.work[i] = d.batch_isend_irecv([self._p2p(d.irecv, self.recv[i][r], r) for r in range(1, self.world)])
             self.unresolved.append(step)
             return
         self._wait(i)  # the buffer's previous transfer (step - 2)
@@ -296,9 +329,9 @@ class RecordGather:
         if self.cuda:
             self.copied[i] = torch.cuda.Event()
             self.copied[i].record()
-        self.work[i] = d.batch_isend_irecv([d.P2POp(d.isend, self.send[i], 0)])
+        self.work[i] = d.batch_isend_irecv([self._p2p(d.isend, self.send[i], 0)])
         if n_over:
-            self.owork[i] = d.batch_isend_irecv([d.P2POp(d.isend, self.ovf[i], 0)])
+            self.owork[i] = d.batch_isend_irecv([self._p2p(d.isend, self.ovf[i], 0)])
 
     def result(self, step):
         """Rank 0: {peer: (header [batch, 4 + rec_bytes], overflow bytes or None)}."""
@@ -330,6 +363,88 @@ class RecordGather:
                 self._resolve(self.unresolved.pop(0))
         self._wait(0)
         self._wait(1)
+
+
+class ScatterLoop:
+    """The north-star loop (bench.py ``--ingest scatter``, and the scatter leg of every
+    N > 1 line): frames leave rank 0 by ScatterIngest, every rank detects its batch on
+    detector instances used round-robin (batch k enqueued on instance k mod n, collected
+    n - 1 enqueues later: the local loop's in-flight depth), and each peer's records
+    return to rank 0 by RecordGather -- the first `rec_cap` records of every frame in the
+    fixed-size row plus an overflow message.  The scatter of step k + 1 overlaps the
+    detection of steps k - n + 2 .. k (one frame buffer per instance; a buffer is sent
+    again only after the batch that read it is collected).
+
+    A detector here is anything with GpuDetector's ``enqueue_device(ptr, stride, n)``,
+    ``collect(counts_only=True)``, ``wait_stream``, the page-locked record buffer
+    ``_out_t``, the per-frame counts ``_n`` and ``frame_record_bytes(f)`` (the gloo test
+    stands a CPU detector in)."""
+
+    def __init__(self, dist, dets, ingest, gather, batch: int, stride: int, rec_cap: int):
+        self.dist, self.dets, self.ingest, self.gather = dist, list(dets), ingest, gather
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.batch, self.stride, self.rec_cap = batch, stride, rec_cap
+        self.rec_bytes = rec_cap * _rec_size()
+        self.copied = {}  # detector -> event after the async copy out of its record buffer
+
+    def _gather(self, d, step):
+        import torch
+        if self.world == 1:
+            return
+        if self.rank == 0:
+            self.gather.post(step)
+            return
+        counts = [int(d._n[f]) for f in range(self.batch)]
+        self.gather.post(step, d._out_t.view(self.batch, -1)[:, :self.rec_bytes], torch.tensor(counts, dtype=torch.int32),
+                         overflow_from(counts, self.rec_cap, d.frame_record_bytes))
+        self.copied[id(d)] = self.gather.copied[step % 2]
+
+    def run(self, nsteps: int, step0: int = 0) -> int:
+        """Runs nsteps batches from step step0; returns this rank's detections."""
+        ndet, ni, inflight = 0, len(self.dets), []
+
+        def drain():
+            pd, ps = inflight.pop(0)
+            ev = self.copied.pop(id(pd), None)
+            if ev is not None:  # its record buffer may still be copied from
+                ev.synchronize()
+            n = sum(pd.collect(counts_only=True))
+            self._gather(pd, ps)
+            return n
+
+        self.ingest.start(step0)
+        for s in range(step0, step0 + nsteps):
+            d = self.dets[(s - step0) % ni]
+            buf = self.ingest.ready(s, detector=d)  # stream dependency, no host wait
+            d.enqueue_device(buf.data_ptr(), self.stride, self.batch)
+            inflight.append((d, s))
+            if len(inflight) == ni:
+                ndet += drain()
+            if s + 1 < step0 + nsteps:
+                self.ingest.start(s + 1)  # its buffer was read by step s+1-instances, collected above
+        while inflight:
+            ndet += drain()
+        self.gather.drain()
+        self.ingest.drain()
+        return ndet
+
+
+def scatter_leg_summary(world: int, steps: int, batch: int, frame_bytes: int, elapsed: float, detections: int,
+                        records_at_rank0):
+    """The scatter topology's sub-object of an N > 1 bench line: whole-job frames/s over
+    the leg's timed steps (max elapsed over ranks), what rank 0 holds afterwards, and the
+    bytes each peer received from rank 0 over its xGMI link."""
+    per_step = batch * frame_bytes
+    return {"value": round(world * steps * batch / elapsed, 2), "unit": "frames/s", "steps": steps,
+            "ms_per_step": round(1e3 * elapsed / steps, 4), "detections": int(detections),
+            "records_at_rank0": None if records_at_rank0 is None else int(records_at_rank0),
+            "peers": world - 1, "bytes_scattered_per_peer_per_step": per_step,
+            "bytes_scattered_per_peer": per_step * steps,
+            "GBps_per_peer": round(per_step * steps / elapsed / 1e9, 3),
+            "note": "north-star topology (SURVEY.md 8(e)): frames resident on rank 0, each step's batch sent to "
+                    "every peer by RCCL point-to-point (multigpu.ScatterIngest), detection records gathered to "
+                    "rank 0 (multigpu.RecordGather: a 32-record row per frame + overflow); rank 0's own share "
+                    "read in place"}
 
 
 def reduce_max_sum(dist, elapsed: float, count: float, device):

@@ -276,3 +276,111 @@ def test_record_gather_keeps_dense_frames_world2():
                 for key in ("H", "c", "p"):
                     assert np.array_equal(np.asarray(a[key]).ravel(), np.asarray(b[key], np.float64).ravel())
     assert nrec == 3 * (2 * 131 + 15)
+
+
+def _leg_dets(v):
+    """What the stand-in detector finds in a frame filled with byte v: (v % 3) records,
+    plus 40 more when v % 4 == 1 (above the 32-record row: the overflow message)."""
+    n = v % 3 + (40 if v % 4 == 1 else 0)
+    return [dict(id=100 * v + k, hamming=k % 3, decision_margin=float(k), H=np.eye(3) * v, c=np.array([v, k]),
+                 p=np.full((4, 2), 0.25 * k)) for k in range(n)]
+
+
+class _CpuDetector:
+    """GpuDetector's interface as multigpu.ScatterLoop drives it (enqueue_device on a
+    frame buffer's address, collect, the page-locked record buffer _out_t with 64
+    records per frame, _n, frame_record_bytes), detecting on the CPU by _leg_dets."""
+
+    def __init__(self, batch, rs):
+        import torch
+        self.batch, self.rs, self.cap = batch, rs, 64
+        self._out_t = torch.zeros(batch * self.cap * rs, dtype=torch.uint8)
+        self._n = [0] * batch
+        self.seen = []
+
+    def enqueue_device(self, ptr, stride, n):
+        import ctypes
+        buf = np.ctypeslib.as_array((ctypes.c_uint8 * (stride * n)).from_address(ptr)).reshape(n, stride)
+        self._pending = [int(buf[f, 0]) for f in range(n)]
+        assert all((buf[f] == buf[f, 0]).all() for f in range(n))
+
+    def collect(self, counts_only=True):
+        import torch
+        from ros_vision_amd import multigpu
+        for f, v in enumerate(self._pending):
+            dets = _leg_dets(v)
+            rec = multigpu.detection_records(dets)[:len(dets) * self.rs]
+            o = f * self.cap * self.rs
+            if rec:
+                self._out_t[o:o + len(rec)] = torch.frombuffer(bytearray(rec), dtype=torch.uint8)
+            self._n[f] = len(dets)
+            self.seen.append(v)
+        return list(self._n)
+
+    def frame_record_bytes(self, f):
+        o = f * self.cap * self.rs
+        return bytes(self._out_t[o:o + self._n[f] * self.rs].numpy())
+
+
+def _leg_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from ros_vision_amd import multigpu
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, npool, shape, ni, steps = 3, 9, (4, 8), 2, 7
+    pool = None
+    if rank == 0:  # frame (r, i) is filled with 16 r + i
+        pool = torch.stack([torch.stack([torch.full(shape, 16 * r + i, dtype=torch.uint8) for i in range(npool)])
+                            for r in range(world)])
+    ingest = multigpu.ScatterIngest(dist, pool, B, shape, "cpu", nbuf=ni)
+    gather = multigpu.RecordGather(dist, B, 32 * multigpu._rec_size(), "cpu")
+    dets = [_CpuDetector(B, multigpu._rec_size()) for _ in range(ni)]
+    loop = multigpu.ScatterLoop(dist, dets, ingest, gather, B, shape[0] * shape[1], 32)
+    loop.run(ni, 0)  # warm-up, as bench.py's leg
+    recv0 = gather.records_received
+    nd = loop.run(steps, step0=ni)
+    at_root = nd + gather.records_received - recv0 if rank == 0 else None
+    el, tot = multigpu.reduce_max_sum(dist, 0.5 + rank, nd, "cpu")
+    leg = multigpu.scatter_leg_summary(world, steps, B, shape[0] * shape[1], el, tot, at_root)
+    q.put((rank, leg, sorted(v for d in dets for v in d.seen)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_scatter_leg_world2():
+    """the N > 1 bench line's scatter leg (multigpu.ScatterLoop, the
+    loop bench.py --ingest scatter runs): every rank detects exactly the frames rank 0
+    holds for it, step after step, and rank 0 ends with every record of every rank
+    (frames above the 32-record row included); the sub-object's fields."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_leg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (leg, seen) for r, leg, seen in (q.get(timeout=300) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    B, npool, ni, steps = 3, 9, 2, 7
+    want_total = 0
+    for r in range(world):
+        want = []
+        for s in list(range(ni)) + list(range(ni, ni + steps)):
+            off = (s * B) % npool
+            off = 0 if off + B > npool else off
+            want += [16 * r + off + k for k in range(B)]
+        assert res[r][1] == sorted(want)
+        want_total += sum(len(_leg_dets(16 * r + ((s * B) % npool) + k)) for s in range(ni, ni + steps) for k in range(B))
+    leg = res[0][0]
+    assert leg["records_at_rank0"] == leg["detections"] == want_total
+    assert any(v % 4 == 1 for v in res[1][1])  # (a peer frame went through the overflow message)
+    assert leg["steps"] == steps and leg["peers"] == 1 and leg["unit"] == "frames/s"
+    assert leg["bytes_scattered_per_peer_per_step"] == B * 32
+    assert leg["bytes_scattered_per_peer"] == steps * B * 32
+    assert abs(leg["value"] - world * steps * B / 1.5) < 0.01  # max elapsed over ranks (1.5 s)
+    assert res[1][0]["records_at_rank0"] is None

@@ -110,6 +110,56 @@ def test_c4_1080p_throughput_mode(oracle_mod):
         assert compare_detections(res[f], orc.detections()) == []
 
 
+def test_bench_1080p_configuration():
+    """configs[3]'s per-GPU workload at the bench's own settings:
+    1920x1080, the batch, instances, HBM pool copies and DOMINANT kernel timer that
+    `bench.py --width 1920 --height 1080 --tags 24` uses (imported from bench.py), so
+    the 1080p throughput kernels (CAP-8192 teams for the blobs over 4096 points, the
+    mid-size 128-thread teams, k_ccl_merge at 1080p) run at B = 192 with four batches
+    in flight, graph replay then the split timer graphs.  The 8 C4 golden frames are
+    tiled to a 64-frame pool; every frame of every batch against the goldens."""
+    import torch
+
+    import bench
+    import make_stream_golden as mg
+    import ros_vision_amd as rva
+    from ros_vision_amd.stream import StreamRunner
+    g = load_stream_golden("c4")
+    frames8 = mg.c4_frames(dict(rva.family_entries()))
+    assert [mg.digest(f) for f in frames8] == list(g["frame_digest"])
+    args = bench.parse(["--width", "1920", "--height", "1080", "--tags", "24"])
+    instances, B, copies, timed = args.instances, args.batch, bench.pool_copies(args), bench.DOMINANT
+    assert B >= 128 and instances >= 2
+    pool = args.pool
+    frames = np.concatenate([frames8] * (pool // 8))
+    d_frames = torch.from_numpy(frames).to("cuda").repeat(copies, 1, 1).contiguous()
+    stride = frames[0].nbytes
+    dets = [rva.GpuDetector(1920, 1080, max_batch=B) for _ in range(instances)]
+    runner = StreamRunner(dets, d_frames.data_ptr(), stride, pool * copies, B)
+    bad, seen = [], {"frames": 0, "dets": 0}
+    want = int(np.sum(g["ndet"][:8]))
+
+    def check(det, step, off):
+        res = det.results()
+        for j in range(B):
+            f = (off + j) % 8
+            assert det.frame_status(j) == 0
+            bad.extend(compare_with_stream_golden(g, f, res[j], det.poses(j)))
+            seen["dets"] += len(res[j])
+        seen["frames"] += B
+
+    n1 = runner.run(instances, 0, on_batch=check)
+    assert bad == [], bad[:10]
+    for d in dets:
+        d.set_kernel_timer(timed)
+    n2 = runner.run(instances, instances, on_batch=check)
+    assert bad == [], bad[:10]
+    assert all(launches == 1 for _, launches in (d.kernel_span() for d in dets))
+    for d in dets:
+        d.set_kernel_timer(None)
+    assert seen["frames"] == 2 * instances * B and n1 + n2 == seen["dets"] == 2 * instances * B // 8 * want > 0
+
+
 def test_host_ingest_loop(c2):
     """bench.py's host_ingest leg: the same round-robin loop fed from page-locked
     host frames through at_enqueue_host (H2D copies on the detector streams, runs of
