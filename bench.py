@@ -34,12 +34,14 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec + p50 per-frame latency, 1280x720 AprilTag detect at 1/2/4/8 MI355X"
 # The roofline's kernel, by a fixed rule rather than by the stage profile of the box
-# (the top serialized stages are within ~10 % of each other and swapped places
-# between boxes): the kernel with the largest marginal cost in the concurrent bench
-# loop -- throughput with the sequence cut after each stage (tools/ablate.sh,
-# profiles/r04c/ablation.txt: k_thr_ccl 0.235 ms of 1.23 ms per step, then
-# k_boundary 0.222, k_blob_small 0.185).
+# (the top serialized stages are within ~10 % of each other and swap places between
+# boxes): the kernel with the largest marginal cost in the concurrent bench loop --
+# throughput with the launch sequence cut after each stage (AT_DIAG_PIPE_STOP,
+# tools/r06_call.sh ABL=1), re-derived at HEAD and committed as ABLATION; every line
+# reports that file's marginal costs and flags a DOMINANT that no longer matches it
+# (tests/test_bench_cli.py checks the pair).
 DOMINANT = "k_thr_ccl"
+ABLATION = "profiles/r06/ablation_720p.txt"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -106,6 +108,30 @@ def pool_copies(args):
     if args.hbm_copies:
         return max(1, args.hbm_copies)
     return max(4, -(-2 * args.batch // args.pool))
+
+
+STAGE_NAMES = ["k_pre", "k_thr_ccl", "k_ccl_merge", "k_ccl_roots", "k_boundary", "k_pairs", "k_group", "k_extents",
+               "k_blob_small", "k_blob", "k_decode", "k_pose"]  # (at_common.h kStageNames)
+
+
+def ablation_marginals(path=None):
+    """Marginal ms per step of each stage from a stage-cut ablation file (lines
+    `pipe_stop=N frames/s ms_per_step ...`: only the stages < N launched): the stage
+    added by a cut at N over the previous cut is STAGE_NAMES[N - 1] (the stages between
+    them are not launched in throughput mode: k_ccl_roots).  Returns ({stage: ms}, top)."""
+    path = os.path.join(ROOT, path or ABLATION)
+    ms = {}
+    for line in open(path):
+        f = line.split()
+        if f and f[0].startswith("pipe_stop=") and len(f) >= 3:
+            n = int(f[0].split("=")[1])
+            if n > 0:
+                ms[n] = float(f[2])
+    out, prev = {}, 0.0
+    for n in sorted(ms):
+        out[STAGE_NAMES[n - 1]] = round(ms[n] - prev, 4)
+        prev = ms[n]
+    return out, max(out, key=out.get)
 
 
 def kernel_algorithmic_bytes(kernel, stats, W, H):
@@ -551,6 +577,14 @@ def main():
     # the concurrent loop) with its launch measured in isolation (one batch in flight),
     # its device-clock span in this run; the longest isolated kernel is named beside it
     iso_rows = isolated_table(iso, W, H)
+    try:
+        marg, abl_top = ablation_marginals()
+        ablation = {"file": ABLATION, "marginal_ms_per_step": marg, "top_stage": abl_top,
+                    "dominant_changed": abl_top != DOMINANT,
+                    "note": "stage-cut ablation at the bench configuration (%d instances x %d frames, 720p): "
+                            "ms per step added by each stage; DOMINANT is its top stage" % (4, 192)}
+    except OSError:
+        ablation = None
     head = next((r for r in iso_rows if r["kernel"] == dominant), None)
     longest = iso_rows[0]["kernel"] if iso_rows else None
     # concurrent: the DOMINANT kernel timed inside the timed region (four batches in flight)
@@ -567,7 +601,7 @@ def main():
                     "longest_isolated_kernel": longest, "differs_from_longest_isolated": longest != head["kernel"],
                     "isolated": iso_rows,
                     "note": "DOMINANT (fixed rule: the largest marginal cost in the concurrent loop, "
-                            "profiles/r04c/ablation.txt) measured in isolation in this run: one batch of "
+                            "%s, see `ablation`) measured in isolation in this run: one batch of "
                             "%d frames in flight (enqueue, collect), the kernel timer on one kernel at a time, "
                             "avg_launch_ms = its execution span on the device wall clock (first workgroup start "
                             "to last workgroup end, at_kernel_span: what a rocprofv3 kernel trace reports; "
@@ -575,7 +609,7 @@ def main():
                             "profiles/); algorithmic bytes per DESIGN.md section 4; traffic = PMC "
                             "(2*FETCH_SIZE+WRITE_SIZE) per launch from profiles/pmc_traffic.json; `isolated`: "
                             "every kernel the same way, longest first (the top three are within ~10 %% of each "
-                            "other and change places between boxes)" % B}
+                            "other and change places between boxes)" % (ABLATION, B)}
     else:
         roofline = None
     roofline_concurrent = {
@@ -588,7 +622,7 @@ def main():
         "frac_hip_events": round(kbytes / (k_ms_events * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
         if (kbytes and k_ms_events > 0) else None,
         "top_serialized_stage": top_stage, "differs_from_top_serialized_stage": bool(top_stage and top_stage != dominant),
-        "note": "DOMINANT (fixed rule: the largest marginal cost in the concurrent loop, profiles/r04c/ablation.txt) "
+        "note": "DOMINANT (fixed rule: the largest marginal cost in the concurrent loop, " + ABLATION + ") "
                 "timed on every launch of the timed region with %d batches in flight: its span there holds the "
                 "other batches' kernels sharing the CUs (co-residency), and a tracer changes how the batches "
                 "interleave, so this figure is not reproducible under rocprofv3; top_serialized_stage = the "
@@ -642,6 +676,7 @@ def main():
                              for k in ("host_wait_us_total", "host_tail_us_total")},
         "stage_ms_per_batch": {k: round(v, 4) for k, v in stages.items()},
         "dominant_kernel": dominant,
+        "ablation": ablation,
         "pipeline_gpu_ms_per_batch": round(pipe_ms, 4) if pipe_ms else None,
         "cpu_baseline": None,
     }

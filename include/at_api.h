@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define AT_ABI_VERSION 4
+#define AT_ABI_VERSION 5
 
 enum {
   AT_OK = 0,
@@ -267,6 +267,14 @@ int at_draw_outlines_device(at_detector *d, const at_detection *dets, int n, uin
  * (width x height x 3) to `bgr_out` in host memory.  AT_E_INVALID unless the last
  * batch was host BGR8 frames.  The staged copy is consumed (overwritten). */
 int at_annotate_staged(at_detector *d, int frame, const at_detection *dets, int n, uint8_t *bgr_out);
+
+/* Page-locked host memory (hipHostMalloc) for buffers the detector copies into on
+ * its stream by DMA, e.g. at_annotate_staged's bgr_out: a pageable destination
+ * goes through the runtime's staging buffers instead.  (No counterpart in the
+ * reference: its node copies the image with cv_bridge, apriltags_cuda_detector.cu:514-518.)
+ * Returns AT_OK / AT_E_NOMEM; at_host_free(NULL) is a no-op. */
+int at_host_alloc(size_t bytes, void **out);
+void at_host_free(void *p);
 
 void at_destroy(at_detector *d);
 const char *at_strerror(int code);

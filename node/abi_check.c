@@ -12,7 +12,7 @@
 
 #include "../include/at_api.h"
 
-_Static_assert(AT_ABI_VERSION == 4, "at_api.h ABI version");
+_Static_assert(AT_ABI_VERSION == 5, "at_api.h ABI version");
 _Static_assert(sizeof(at_camera) == 72, "at_camera");
 _Static_assert(sizeof(at_config) == 72, "at_config");
 _Static_assert(offsetof(at_config, family) == 8 && offsetof(at_config, decode_sharpening) == 24 &&

@@ -127,7 +127,7 @@ int main(int argc, char** argv) {
     core.publish_camera = on_camera;
     core.ctx = &sink;
     at_node::FrameOutputs out;
-    std::vector<uint8_t> image;
+    at_node::ImageBuffer image;
     if (time_n > 0) {  // the node's per-frame path, timed
       std::vector<double> ms, det_ms;
       for (int it = -count; it < time_n; ++it) {  // (the first pass over the frames is warm-up)

@@ -492,7 +492,7 @@ DetectorCore::~DetectorCore() {
 }
 
 int DetectorCore::process(const uint8_t* frame, at_pixfmt fmt, double stamp_s, double receive_s, FrameOutputs* out,
-                          std::vector<uint8_t>* annotate) {
+                          ImageBuffer* annotate) {
   using clk = std::chrono::steady_clock;
   auto us = [](clk::time_point a, clk::time_point b) {
     return (long long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
@@ -540,7 +540,8 @@ int DetectorCore::process(const uint8_t* frame, at_pixfmt fmt, double stamp_s, d
       image_queue_.reset(new PublisherQueue<StampedImage>(
           [pub, c](const StampedImage& img) { pub(c, img.bgr, img.stamp_s); }, 2));
     }
-    image_queue_->enqueue(StampedImage{*annotate, stamp_s});  // image_pub_queue_->enqueue (:514-518)
+    // image_pub_queue_->enqueue (:514-518): the queue owns a copy
+    image_queue_->enqueue(StampedImage{std::vector<uint8_t>(annotate->begin(), annotate->end()), stamp_s});
   }
   const auto pi1 = clk::now();
   if (csv_) {  // latency,det,publish_pose,publish_camera_pose,publish_image,networktables,processing (:526-552)

@@ -25,6 +25,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -32,6 +33,28 @@
 #include "../include/at_api.h"
 
 namespace at_node {
+
+// Page-locked allocation (at_host_alloc) for the annotated image: at_annotate_staged
+// then copies it out of HBM by DMA on the detector's stream instead of through the
+// runtime's staging of a pageable destination.
+template <class T>
+struct PinnedAllocator {
+  using value_type = T;
+  PinnedAllocator() = default;
+  template <class U>
+  PinnedAllocator(const PinnedAllocator<U>&) {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    if (at_host_alloc(n * sizeof(T), &p) != AT_OK || !p) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { at_host_free(p); }
+  template <class U>
+  bool operator==(const PinnedAllocator<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAllocator<U>&) const { return false; }
+};
+using ImageBuffer = std::vector<uint8_t, PinnedAllocator<uint8_t>>;
 
 // Node parameters with the reference defaults (apriltags_cuda_detector.cu:93-133, :558-593).
 struct Params {
@@ -206,7 +229,7 @@ class DetectorCore {
   // on the GPU on the frame already staged in HBM (at_annotate_staged); publish_image
   // then gets it from the drop-oldest PublisherQueue thread (depth 2, :50-52, :518).
   int process(const uint8_t* frame, at_pixfmt fmt, double stamp_s, double receive_s, FrameOutputs* out,
-              std::vector<uint8_t>* annotate = nullptr);
+              ImageBuffer* annotate = nullptr);
 
   const Params& params() const { return params_; }
   int width() const { return width_; }

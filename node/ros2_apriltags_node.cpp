@@ -140,7 +140,8 @@ class ApriltagsAmdNode : public rclcpp::Node {
   }
 
   int width_ = 0, height_ = 0;
-  std::vector<uint8_t> packed_, image_;
+  std::vector<uint8_t> packed_;
+  at_node::ImageBuffer image_;  // page-locked: the annotated image arrives by DMA
   rclcpp::Publisher<apriltags_cuda::msg::TagDetectionArray>::SharedPtr pose_pub_, camera_pose_pub_;
   rclcpp::Publisher<sensor_msgs::msg::Image>::SharedPtr image_pub_;
   // after the publishers: destroyed first (members go in reverse order), so the

@@ -327,7 +327,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   // frames list ~40), at most what 160 KiB hold; latency mode keeps the
   // multi-workgroup border / roots kernels (one frame: their parallelism is the chain)
   g.merge_cap = g.ctw == 64 ? std::min(kMergeCapMax, 80 * g.CTX * g.CTY) : 0;
-  g.merge_lds = std::min(g.merge_cap * 14, kMergeLdsMax);
+  // 12 B per root (parent key + pixel count) and the wave link lists (8 KB)
+  g.merge_lds = std::min(g.merge_cap * 12 + 8192, kMergeLdsMax);
   if (g.CTX * g.CTY > kMaxCclTiles) {
     at_destroy(d);
     return AT_E_INVALID;
@@ -1051,7 +1052,8 @@ static void outline_prims(const at_detection* dets, int n, std::vector<DrawPrim>
   }
 }
 
-int at_draw_outlines_device(at_detector* d, const at_detection* dets, int n, uint8_t* bgr) {
+// the outline segments drawn onto `bgr` on the detector's stream (not waited for)
+static int draw_outlines(at_detector* d, const at_detection* dets, int n, uint8_t* bgr) {
   if (!d || n < 0 || (n > 0 && !dets) || !bgr) return AT_E_INVALID;
   HIPCHK(hipSetDevice(d->device));
   std::vector<DrawPrim> prims;
@@ -1072,6 +1074,12 @@ int at_draw_outlines_device(at_detector* d, const at_detection* dets, int n, uin
   }
   HIPCHK(hipMemcpyAsync(d->d_prims, prims.data(), prims.size() * sizeof(DrawPrim), hipMemcpyHostToDevice, d->st));
   HIPCHK(launch_draw(d->d_prims, (int)prims.size(), d->d_last, bgr, (int)W, (int)H, d->st));
+  return AT_OK;
+}
+
+int at_draw_outlines_device(at_detector* d, const at_detection* dets, int n, uint8_t* bgr) {
+  const int rc = draw_outlines(d, dets, n, bgr);
+  if (rc != AT_OK) return rc;
   HIPCHK(hipStreamSynchronize(d->st));
   return AT_OK;
 }
@@ -1082,10 +1090,27 @@ int at_annotate_staged(at_detector* d, int frame, const at_detection* dets, int 
   HIPCHK(hipSetDevice(d->device));
   if (d->pending) HIPCHK(hipEventSynchronize(d->ev_done));
   uint8_t* img = d->d_in + (size_t)frame * d->in_stride;
-  const int rc = at_draw_outlines_device(d, dets, n, img);
+  const int rc = draw_outlines(d, dets, n, img);
   if (rc != AT_OK) return rc;
-  HIPCHK(hipMemcpy(bgr_out, img, (size_t)d->g.W * d->g.H * 3, hipMemcpyDeviceToHost));
+  // in stream order after the drawing, on the detector's stream (no null-stream copy);
+  // DMA straight into a page-locked bgr_out (at_host_alloc)
+  HIPCHK(hipMemcpyAsync(bgr_out, img, (size_t)d->g.W * d->g.H * 3, hipMemcpyDeviceToHost, d->st));
+  HIPCHK(hipStreamSynchronize(d->st));
   return AT_OK;
+}
+
+int at_host_alloc(size_t bytes, void** out) {
+  if (!out) return AT_E_INVALID;
+  *out = nullptr;
+  if (hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return AT_E_NOMEM;
+  }
+  return AT_OK;
+}
+
+void at_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 // ---- shared game-piece preprocessing ---------------------

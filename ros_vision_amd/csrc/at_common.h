@@ -52,8 +52,8 @@ struct CclDesc {
   static constexpr int LsF = 144, LsL = 152, RsF = 160, RsR = 168;
   static constexpr int kWords = 176;
 };
-// k_ccl_merge's LDS: 14 B per listed local root (parent key, tile, pixel count), or
-// 10 B for frames with more roots (counts summed at L2)
+// k_ccl_merge's LDS: 12 B per listed local root (parent key, pixel count), or 10 B
+// (parent key, tile) for frames with more roots (counts summed at L2)
 // next to the per-tile prefix, within the 160 KiB one workgroup may hold
 constexpr int kMergeCapMax = 15360;
 constexpr int kMergeLdsMax = kMergeCapMax * 10;  // (+ the per-tile prefix: within 160 KiB)
@@ -133,7 +133,7 @@ struct Geom {
   int CTX, CTY;         // CCL tiles
   int ctw;              // CCL tile width (32: latency mode, 64: throughput mode)
   int merge_cap;        // k_ccl_merge: listed local roots one frame's LDS holds (0: no k_ccl_merge)
-  int merge_lds;        // k_ccl_merge's dynamic LDS bytes (14 B per root up to kMergeLdsMax)
+  int merge_lds;        // k_ccl_merge's dynamic LDS bytes (12 B per root + link lists, up to kMergeLdsMax)
   int nlarge;           // size classes 0 .. nlarge-1 go to the workgroup-team blob kernel
   int bnd_region;       // points per k_boundary tile region (kBndPts)
   int cap_pts;          // 4 * (Wd-2) * (Hd-2)

@@ -380,15 +380,6 @@ __device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
 }
 // find with path halving: every visited node is pointed at its grandparent (an
 // ancestor with a smaller id, so the atomicMin never loses a link)
-#ifndef AT_CCL_LEAN_SYNC
-#define AT_CCL_LEAN_SYNC 1
-#endif
-#ifndef AT_CCL_UNION_LIST
-#define AT_CCL_UNION_LIST 1
-#endif
-#ifndef AT_CCL_HEAD_FIND
-#define AT_CCL_HEAD_FIND 1
-#endif
 __device__ __forceinline__ uint32_t lds_find(uint32_t* par, uint32_t n) {
   uint32_t p = lds_load(par + n);
   while (p != n) {
@@ -701,9 +692,6 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   for (int i = tid; i < kCclTileNodes; i += NT) s_cnt[i] = 0;
   __syncthreads();
   ph(3);
-#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
-  if (AT_THR_CUT == 1) return;
-#endif
 
   // write this tile's threshold plane (4 bytes per thread)
   {
@@ -774,10 +762,8 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     // compression runs is a node of the same component -- unions and compressions only
     // lower a parent within its component -- so the union it takes part in is still the
     // right one; a changed value only defeats the left-neighbour dedup, an extra union)
-    if (!AT_CCL_LEAN_SYNC) __syncthreads();
   ph(5);
     auto seen_fg = [&](uint32_t t) { return fg_left && (t == pUL || t == pU || t == pUR); };
-#if AT_CCL_UNION_LIST
     // the wave's unions (at most five per block, mostly none) compacted into a
     // wave-private list in s_gid's storage (unused until the publish) and run with
     // every lane busy: ceil(n / 64) union rounds instead of five divergent sites in a
@@ -808,22 +794,11 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     push(tL != kNone && !(bg_left && tL == pR), hL, tL);
     push(tR != kNone && !(bg_in && tR == tL), hR, tR);
     if (nq) flush();
-#else
-    if (tUL != kNone && !seen_fg(tUL)) lds_union(s_par, hF, tUL);
-    if (tU != kNone && tU != tUL && !seen_fg(tU)) lds_union(s_par, hF, tU);
-    if (tUR != kNone && tUR != tUL && tUR != tU && !seen_fg(tUR)) lds_union(s_par, hF, tUR);
-    if (tL != kNone && !(bg_left && tL == pR)) lds_union(s_par, hL, tL);
-    if (tR != kNone && !(bg_in && tR == tL)) lds_union(s_par, hR, tR);
-#endif
   }
 #undef T
   __syncthreads();
   ph(6);
-#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
-  if (AT_THR_CUT == 2) return;
-#endif
 
-#if AT_CCL_HEAD_FIND
   // Every find path runs through run heads only (a run's other nodes point at its head,
   // and unions and path halving only ever link heads), so only the heads are found --
   // compacted per wave like the unions, with no barrier before the root writes (a root
@@ -851,18 +826,6 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   }
   const uint32_t rF = s_par[s_par[F]], rL = s_par[s_par[L]], rR = s_par[s_par[R]];
   ph(7);
-#else
-  (void)headF; (void)headL; (void)headR;
-  const uint32_t rF = lds_find(s_par, F), rL = lds_find(s_par, L), rR = lds_find(s_par, R);
-  // (no barrier before the root writes: each writes a node's final root -- the smallest
-  // slot of its component, so a concurrent compression's atomicMin leaves it -- and a
-  // find that reads it lands on that root)
-  if (!AT_CCL_LEAN_SYNC) __syncthreads();
-  ph(7);
-  s_par[F] = rF;
-  s_par[L] = rL;
-  s_par[R] = rR;
-#endif
   // every slot's global node id, by its owner (the publish looks its roots' ids up
   // instead of decoding slot numbers: ~15 VALU per decode)
   const uint32_t idF = (uint32_t)(2 * (y0 / 2 + bty) * g.Wd + 2 * (x0 / 2 + btx)), idL = idF + g.Wd;
@@ -895,9 +858,6 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   count(rR, nbr);
   __syncthreads();
   ph(8);
-#ifdef AT_THR_CUT  // (diagnostic builds, with AT_DIAG_PIPE_STOP=2: where k_thr_ccl's time goes)
-  if (AT_THR_CUT == 3) return;
-#endif
 
   // publish: gpar[node] = global id of its local root; size[root] = local pixel count
   const int BY = y0 / 2 + bty, BX = x0 / 2 + btx;
@@ -1181,9 +1141,6 @@ __global__ __launch_bounds__(64) void k_ccl_roots(DevBufs b, Geom g) {
 // workgroup in global memory (k_ccl_border's unions, k_ccl_roots' pass, the kept
 // bits; ccl_ovf set).
 // ---------------------------------------------------------------------------
-#ifndef AT_MERGE_UNION_LIST
-#define AT_MERGE_UNION_LIST 1
-#endif
 constexpr int kMergeList = 64;  // link pairs per wave list (k_ccl_merge)
 constexpr int kMergePer = (kMergeCapMax + 1023) / 1024;  // listed roots per thread
 constexpr int kMergeItems = 2;                          // border blocks per thread per pass
@@ -1233,11 +1190,14 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
   using CT = CclTile<TWD>;
   constexpr int kBW = CT::BW, kBH = CT::BH;
   // LDS laid out by the frame's number of listed roots (total): parent keys (gid << 32 |
-  // slot), the tile of each slot and, when 14 B per root fit, the pixel counts; a frame
-  // whose counts do not fit (1080p noise: ~11 k roots) sums them in the size plane at L2
-  // instead (10 B per root: up to 15,360 roots)
+  // slot) and, when 12 B per root fit (up to 12,799 roots: 1080p stream frames list
+  // ~11 k), the pixel counts -- the roots are then visited a wave per tile, so no slot
+  // needs its tile; a frame whose counts do not fit (1080p noise) keeps the tile of each
+  // slot and sums the counts in the size plane at L2 instead (10 B per root: up to
+  // 15,360 roots).  (Counts at L2 for the ~11 k roots of a 1080p stream frame: the
+  // root-word pass read them back at 53 us per frame, profiles/r06c.)
   extern __shared__ uint64_t s_key[];          // [total] parent key
-  uint16_t* s_tile = nullptr;                  // [total] tile of each slot
+  uint16_t* s_tile = nullptr;                  // [total] tile of each slot (!cnt_lds)
   uint32_t* s_cnt = nullptr;                   // [total] pixel counts (cnt_lds)
   __shared__ uint32_t s_base[kMaxCclTiles + 1];
   __shared__ uint32_t s_wsum[16];
@@ -1264,11 +1224,11 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     b.nlr_tot[f] = total;
   }
   const bool fits = total <= (uint32_t)g.merge_cap;
-  const bool cnt_lds = (size_t)total * 14 + 4 <= (size_t)g.merge_lds;
+  const bool cnt_lds = (size_t)total * 12 + 4 <= (size_t)g.merge_lds;
   s_tile = reinterpret_cast<uint16_t*>(s_key + total);
-  s_cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_key) + (((size_t)total * 10 + 3) & ~(size_t)3));
+  s_cnt = reinterpret_cast<uint32_t*>(s_key + total);
   __syncthreads();  // s_base complete
-  if (fits)
+  if (fits && !cnt_lds)
     for (int t = tid >> 6; t < ntl; t += 16) {  // a wave per tile
       const uint32_t b0 = s_base[t], n = s_base[t + 1] - b0;
       for (uint32_t k = lane_id(); k < n; k += 64) s_tile[b0 + k] = (uint16_t)t;
@@ -1327,16 +1287,26 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
   // (1) the listed roots: node id and local pixel count (k_thr_ccl's lists)
   const uint32_t* lcnt = b.lcnt + (size_t)f * ntl * kCclTileNodesMax;
   uint32_t mg[kMergePer];
+  if (cnt_lds) {  // a wave per tile (slot = tile base + list index)
+    for (int t = tid >> 6; t < ntl; t += 16) {
+      const uint32_t b0 = s_base[t], n = s_base[t + 1] - b0;
+      for (uint32_t k = lane_id(); k < n; k += 64) {
+        const size_t e = (size_t)t * kCclTileNodesMax + k;
+        s_cnt[b0 + k] = lcnt[e];
+        s_key[b0 + k] = ((uint64_t)lroot[e] << 32) | (b0 + k);
+      }
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < kMergePer; j++) {
-    const uint32_t i = tid + 1024u * j;
-    mg[j] = 0;
-    if (i < total) {
-      const int t = s_tile[i];
-      const size_t e = (size_t)t * kCclTileNodesMax + (i - s_base[t]);
-      mg[j] = lroot[e];
-      if (cnt_lds) s_cnt[i] = lcnt[e];
-      s_key[i] = ((uint64_t)mg[j] << 32) | i;
+    for (int j = 0; j < kMergePer; j++) {
+      const uint32_t i = tid + 1024u * j;
+      mg[j] = 0;
+      if (i < total) {
+        const int t = s_tile[i];
+        const size_t e = (size_t)t * kCclTileNodesMax + (i - s_base[t]);
+        mg[j] = lroot[e];
+        s_key[i] = ((uint64_t)mg[j] << 32) | i;
+      }
     }
   }
   __syncthreads();
@@ -1355,11 +1325,10 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     return (uint32_t)reinterpret_cast<const uint16_t*>(desc + (size_t)t * CclDesc::kWords + w)[i];
   };
   const int n0 = ntl * kBW, n1 = n0 + ntl * kBH, nitems = n1 + ntl * (kBH - 1);
-#if AT_MERGE_UNION_LIST
   // a wave's links (ten candidate sites per lane per pass) compacted by ballot into a
   // wave-private list and run with every lane busy, as in k_thr_ccl -- in the dynamic
   // LDS past the roots when it has room (the usual frame), else the sites directly
-  const size_t lused = ((((size_t)total * 10 + 3) & ~(size_t)3) + (cnt_lds ? (size_t)total * 4 : 0) + 7) & ~(size_t)7;
+  const size_t lused = (cnt_lds ? (size_t)total * 12 : (size_t)total * 10) + 7 & ~(size_t)7;
   const bool ulist = fits && lused + (size_t)16 * kMergeList * 8 <= (size_t)g.merge_lds;  // (uniform)
   uint32_t* wl = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(s_key) + lused) + (tid >> 6) * (2 * kMergeList);
   const uint32_t wlane = lane_id();
@@ -1370,7 +1339,6 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     wave_sync();
     nl = 0;
   };
-#endif
   for (int j0 = 0; j0 < nitems; j0 += 1024 * kMergeItems) {
     uint32_t su[kMergeItems][5], sv[kMergeItems][5];  // slot pair per link (0xffffffff: none)
 #pragma unroll
@@ -1435,7 +1403,6 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
         const bool on = su[q][k] != 0xffffffffu && sv[q][k] < (uint32_t)total && su[q][k] < (uint32_t)total;
         const uint32_t pair = on ? (su[q][k] << 16 | sv[q][k]) : 0xffffffffu;
         const uint32_t prev = wave_shr1(pair, 0xfffffffeu);
-#if AT_MERGE_UNION_LIST
         if (ulist) {
           const bool act = on && pair != prev;
           const uint64_t m = __ballot(act);
@@ -1449,13 +1416,10 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
           nl += c;
           continue;
         }
-#endif
         if (on && pair != prev) merge_union(s_key, su[q][k], sv[q][k]);
       }
   }
-#if AT_MERGE_UNION_LIST
   if (ulist && nl) lflush();
-#endif
   __syncthreads();
   stamp(3);
   // (3) component sizes at the roots: in LDS, or (counts not in LDS) every listed non-root
@@ -1480,15 +1444,28 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
   __syncthreads();
   stamp(4);
   // (4) every listed root's word: root | kept; the root's count: its component's size
+  if (cnt_lds) {  // a wave per tile, the node ids read again from the tile's list (L2)
+    for (int t = tid >> 6; t < ntl; t += 16) {
+      const uint32_t b0 = s_base[t], n = s_base[t + 1] - b0;
+      for (uint32_t k = lane_id(); k < n; k += 64) {
+        const uint32_t node = lroot[(size_t)t * kCclTileNodesMax + k];
+        const uint32_t i = b0 + k;
+        const uint32_t r = merge_find(s_key, i);  // (one hop after (3)'s halving, mostly)
+        const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
+        const uint32_t cnt = s_cnt[r];
+        par[node] = root | (cnt >= 25 ? kKeptBit : 0u);
+        if (r == i) size[node] = cnt;
+      }
+    }
+  } else {
 #pragma unroll
-  for (int j = 0; j < kMergePer; j++) {
-    const uint32_t i = tid + 1024u * j;
-    if (i < total) {
-      const uint32_t r = merge_find(s_key, i);  // (one hop after (3)'s halving, mostly)
-      const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
-      const uint32_t n = cnt_lds ? s_cnt[r] : g_load(size + root);
-      par[mg[j]] = root | (n >= 25 ? kKeptBit : 0u);
-      if (cnt_lds && r == i) size[mg[j]] = n;
+    for (int j = 0; j < kMergePer; j++) {
+      const uint32_t i = tid + 1024u * j;
+      if (i < total) {
+        const uint32_t r = merge_find(s_key, i);
+        const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
+        par[mg[j]] = root | (g_load(size + root) >= 25 ? kKeptBit : 0u);
+      }
     }
   }
   stamp(5);
@@ -1600,12 +1577,6 @@ __device__ __forceinline__ void bnd_spill(const DevBufs& b, int f, uint64_t key,
 #else
 #define AT_BND_ATTR
 #endif
-#ifndef AT_BND_TWO
-#define AT_BND_TWO 1
-#endif
-#ifndef AT_BND_FLAT
-#define AT_BND_FLAT 1
-#endif
 // KEPT (throughput mode): the size test comes with the root word (k_ccl_merge);
 // latency mode skips that kernel and reads the size plane (one more round trip
 // here, one launch less on the chain)
@@ -1679,16 +1650,9 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     }
   }
   __syncthreads();  // LDS tables initialised
-#ifdef AT_BND_CUT  // (diagnostic builds: the staging alone / without the output phase)
-  if (AT_BND_CUT == 1) {
-    if (tid == 0) { b.tcnt[(size_t)f * g.ntb + bi.y * gridDim.x + bi.x] = 0; b.tent[(size_t)f * g.ntb + bi.y * gridDim.x + bi.x] = 0; kt_end(b, 4); }
-    return;
-  }
-#endif
   const uint32_t lane = lane_id();
   const size_t tb = (size_t)f * g.ntb + bi.y * gridDim.x + bi.x;
   uint64_t* pts_out = b.pts + tb * g.bnd_region;
-#if AT_BND_TWO
   // two horizontally adjacent pixels per lane, a wave over two tile rows per step
   // (lanes 0-31 the upper row, 32-63 the lower): the wave-wide work of a step -- the
   // point-offset scan, the pair runs, the staging atomic -- serves 128 pixels.  (Pair
@@ -1715,7 +1679,6 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
 #pragma unroll
       for (int d = 0; d < 4; d++) nb[4 * j + d] = 0;
       const uint32_t v0 = (ra >> (8 * j + 8)) & 0xff;
-#if AT_BND_FLAT
       // branch-free: the five labels read whatever the pixel (the halo holds every
       // address; a label is used only where its direction's bit is set), so no exec-mask
       // region per direction
@@ -1733,20 +1696,6 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
       const uint32_t pm = (v0 + vr == 255 ? 1u : 0u) | (v0 + vdr == 255 ? 2u : 0u) | (v0 + vd == 255 ? 4u : 0u) |
                           (!dedup && v0 + vdl == 255 ? 8u : 0u);
       hm |= pv ? pm << (4 * j) : 0u;
-#else
-      if (xa + j <= g.Wd - 2 && y <= g.Hd - 2 && v0 != 127) {
-        const uint32_t vl = (ra >> (8 * j)) & 0xff, vr = (ra >> (8 * j + 16)) & 0xff;
-        const uint32_t vdl = (rb >> (8 * j)) & 0xff, vd = (rb >> (8 * j + 8)) & 0xff, vdr = (rb >> (8 * j + 16)) & 0xff;
-        const int e0 = eb + j + 1, ed = e0 + kTC;
-        rep[j] = s_tlab[e0];
-        b2w[j] = v0 == 0;
-        if (v0 + vr == 255) { hm |= 1u << (4 * j); nb[4 * j] = s_tlab[e0 + 1]; }
-        if (v0 + vdr == 255) { hm |= 2u << (4 * j); nb[4 * j + 1] = s_tlab[ed + 1]; }
-        if (v0 + vd == 255) { hm |= 4u << (4 * j); nb[4 * j + 2] = s_tlab[ed]; }
-        const bool dedup = vl != 127 && vd != 127 && vd != vl && xa + j != 1;
-        if (!dedup && v0 + vdl == 255) { hm |= 8u << (4 * j); nb[4 * j + 3] = s_tlab[ed - 1]; }
-      }
-#endif
     }
     // pair histogram: the lane's first pair with the count of its points in it (labels
     // are < 2^20 -- decimated planes of at most 1024 x 1024 -- so label equality is
@@ -1819,108 +1768,7 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
         }
     }
   }
-#else
-  const int x = 1 + bi.x * 64 + threadIdx.x;
-  for (int r = 0; r < kBndRows; r++) {
-    const int ly = r * 4 + threadIdx.y;  // tile row of the pixel
-    const int y = ty0 + ly;
-    // the pixel's points: a direction mask and the neighbour labels (the keys are built
-    // only where stored); a point's b2w is v0 == 0 (its neighbour is 255 - v0)
-    uint32_t hm = 0, n0 = 0, n1 = 0, n2 = 0, n3 = 0, rep0 = 0;
-    bool b2w = false;
-    if (x <= g.Wd - 2 && y <= g.Hd - 2) {
-      const int e0 = ly * kTC + threadIdx.x + 1;
-      const uint8_t v0 = s_tthr[e0];
-      if (v0 != 127) {
-        rep0 = s_tlab[e0];
-        b2w = v0 == 0;
-        const int er = e0 + 1, ed = e0 + kTC, edr = ed + 1, edl = ed - 1, el = e0 - 1;
-        const uint8_t vr = s_tthr[er], vd = s_tthr[ed], vdr = s_tthr[edr], vdl = s_tthr[edl], vl = s_tthr[el];
-        if (v0 + vr == 255) { hm |= 1; n0 = s_tlab[er]; }
-        if (v0 + vdr == 255) { hm |= 2; n1 = s_tlab[edr]; }
-        if (v0 + vd == 255) { hm |= 4; n2 = s_tlab[ed]; }
-        const bool dedup = vl != 127 && vd != 127 && vd != vl && x != 1;
-        if (!dedup && v0 + vdl == 255) { hm |= 8; n3 = s_tlab[edl]; }
-      }
-    }
-    const uint32_t nbd[4] = {n0, n1, n2, n3};
-    auto key_of = [&](int dir) { return make_qbp(rep0, nbd[dir], x, y, dir, b2w); };
-    // a direction's pair as the lane sees it (rep0 fixed): the neighbour's side of rep0 and
-    // its 20 key bits -- equal exactly when the directions' 40-bit pair keys are equal
-    auto pid = [&](uint32_t n) { return (n > rep0 ? 0x80000000u : 0u) | (n & 0xfffffu); };
-    uint32_t below = 0, wtot = 0;  // this lane's points below it in the wave, the wave's total
-#pragma unroll
-    for (int dir = 0; dir < 4; dir++) {
-      const uint64_t hmask = __ballot((hm >> dir) & 1);
-      below += lanes_below(hmask);
-      wtot += (uint32_t)__popcll(hmask);
-    }
-    // pair histogram: a pixel's (up to four) points nearly always share one pair,
-    // so a lane adds its first pair with the count of its points in it, runs of
-    // equal pairs in consecutive lanes sum their counts (wave scan), and only the
-    // rare other pairs of a lane go in one by one
-    const bool got = hm != 0;
-    const uint32_t nf = (hm & 1) ? n0 : (hm & 2) ? n1 : (hm & 4) ? n2 : n3;  // first direction's neighbour
-    const uint32_t pf = pid(nf);
-    uint32_t cnt = 0, xm = 0;  // points in the first pair; directions of other pairs
-#pragma unroll
-    for (int dir = 0; dir < 4; dir++) {
-      const bool in = (hm >> dir) & 1, eq = pid(nbd[dir]) == pf;
-      cnt += in && eq;
-      xm |= (in && !eq) ? 1u << dir : 0u;
-    }
-    const uint64_t kp = got ? make_qbp(rep0, nf, 0, 0, 0, false) >> 24 : 0ull;
-    {
-      const uint64_t prev = wave_shr1_u64(kp);
-      const bool same = got && lane > 0 && prev == kp;
-      const uint64_t same_mask = __ballot(same);
-      const uint32_t incl = wave_incl_scan(cnt, AddOp(), 0u);
-      const bool head = got && !same;
-      const uint32_t len = head ? run_len(same_mask, lane) : 1u;
-      const uint32_t incl_end = (uint32_t)__shfl((int)incl, (int)(lane + len - 1));
-      if (head) {
-        const uint32_t tot = incl_end - incl + cnt;
-        if (!lds_pair_add(s_pkey, s_pcnt, kp, tot)) {  // LDS table full
-          bnd_spill(b, f, kp, tot);
-          s_spill = 1;
-        }
-      }
-      if (__ballot(xm != 0)) {
-#pragma unroll
-        for (int dir = 0; dir < 4; dir++) {
-          if ((xm >> dir) & 1) {
-            const uint64_t k = key_of(dir) >> 24;
-            if (!lds_pair_add(s_pkey, s_pcnt, k, 1u)) {
-              bnd_spill(b, f, k, 1u);
-              s_spill = 1;
-            }
-          }
-        }
-      }
-    }
-    // wave-aggregated append of the points into the LDS staging buffer
-    uint32_t wbase = 0;
-    if (lane == 0 && wtot) wbase = atomicAdd(&s_npts, wtot);
-    wbase = __shfl(wbase, 0);
-    uint32_t pos = wbase + below;
-#pragma unroll
-    for (int dir = 0; dir < 4; dir++)
-      if ((hm >> dir) & 1) {
-        const uint64_t k = key_of(dir);
-        if (pos < (uint32_t)kBndStage) s_pts[pos] = k;
-        else if (pos < (uint32_t)g.bnd_region) pts_out[pos] = k;
-        else atomicOr(b.status + f, kStatusPointsOverflow);
-        pos++;
-      }
-  }
-#endif
   __syncthreads();
-#ifdef AT_BND_CUT
-  if (AT_BND_CUT == 2) {
-    if (tid == 0) { b.tcnt[tb] = 0; b.tent[tb] = 0; kt_end(b, 4); }
-    return;
-  }
-#endif
   // the tile's own regions: points and compacted pair entries, plain stores
   // (no per-frame counter: a device-scope atomic per tile on a per-frame
   // address serialized the tiles of a frame)
@@ -4334,18 +4182,14 @@ __device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g,
 }
 
 // K9a (large blobs, > kSmallBlob points): one blob per NT-thread workgroup
-// iteration, persistent over the large work list.  Geometries whose blobs can
-// exceed 4096 points (max_cluster = 2 (W + H) > 4096, e.g. 1080p) run two
-// launches: CAP 4096 (49 KB LDS) over the items of up to 4096 points and CAP
-// 8192 (86 KB, one workgroup per CU) over the few larger ones (nlo = 4096,
-// size class 0 only, its own dequeue head), instead of every large blob in
-// the 86 KB kernel.
-#ifndef AT_MID_BLOB
-#define AT_MID_BLOB 1
-#endif
-#ifndef AT_MID2_NT
-#define AT_MID2_NT 256
-#endif
+// iteration, persistent over the large work list.  Throughput mode: CAP 4096 (49 KB
+// LDS) over the items of 1025-4096 points, CAP 1024 (128 threads) over the 513-1024
+// class, and -- geometries whose blobs can exceed 4096 points (max_cluster = 2 (W + H)
+// > 4096, e.g. 1080p) -- CAP 8192 in 512-thread teams (97 KB, one workgroup per CU)
+// over the few larger ones (nlo = 4096, size class 0 only); each launch dequeues from
+// its own head.  (The 1080p CAP-8192 launch in 256-thread teams, 32 keys per thread,
+// sorted by a bitonic fallback: k_blob 1.68 -> 0.68 ms per 192 frames, 1080p 45.8 k
+// -> 53.0 k frames/s, profiles/r06/ab1080_big_blob_teams.txt.)
 template <int NT, int CAP, bool FUSE = false>
 __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo, int c0, int c1, int launch) {
   __shared__ BlobShared<NT, CAP> S;
@@ -5423,7 +5267,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     } else if (B < kWideBlobMaxBatch || prm.wide_blob) {  // (latency: one launch, longest blob first)
       if (cap4k) hipLaunchKernelGGL((k_blob<512, 4096>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
-    } else if (AT_MID_BLOB) {
+    } else {
       // throughput: blobs of 1025-4096 points (size classes 0 .. nlarge-2) in 256-thread
       // teams, the 513-1024-point class (nlarge-1: two thirds of the large blobs) in
       // 128-thread teams (CAP 1024: the same 8 points per thread as the one-wave kernel;
@@ -5437,9 +5281,6 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
       if (!cap4k)
         hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g,
                            prm, 4096u, 0, 1, 2);
-    } else {
-      hipLaunchKernelGGL((k_blob<256, 4096>), dim3(prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
-      if (!cap4k) hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g, prm, 4096u, 0, 1, 1);
     }
     tk(9, s, 1);
   };

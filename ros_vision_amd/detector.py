@@ -34,7 +34,7 @@ EXPORTS = [
     "at_set_kernel_timer", "at_kernel_time", "at_batch_stats", "at_stream_wait",
     "at_gp_enable", "at_gp_tensor", "at_gp_copy", "at_gp_preprocess_device", "at_set_debug_taps",
     "at_draw_outlines_device", "at_detections", "at_max_detections", "at_annotate_staged", "at_enqueue_host",
-    "at_kernel_span",
+    "at_kernel_span", "at_host_alloc", "at_host_free",
 ]
 
 TAG_SIZE = 0.1651  # metres, apriltags_cuda_detector.hpp:39

@@ -25,3 +25,21 @@ def test_isolated_table_orders_by_span():
     assert rows[0]["algorithmic_bytes_per_launch"] == kb
     assert abs(rows[0]["achieved"] - kb / 0.3e-3 / 1e9) < 1e-3
     assert rows[2]["frac"] is None  # (no algorithmic byte model for k_pairs)
+
+
+def test_dominant_matches_committed_ablation():
+    """DOMINANT is the top stage of the stage-cut ablation committed
+    at bench.ABLATION (marginal ms per step of each stage at the bench configuration)."""
+    marg, top = bench.ablation_marginals()
+    assert top == bench.DOMINANT, marg
+    assert set(marg) >= {"k_pre", "k_thr_ccl", "k_boundary", "k_blob_small", "k_blob", "k_decode"}
+    assert all(v > -0.05 for v in marg.values()), marg
+
+
+def test_ablation_marginals_parse(tmp_path):
+    p = tmp_path / "abl.txt"
+    p.write_text("pipe_stop=0 100 2.0 15\npipe_stop=1 9 0.1 0\npipe_stop=2 8 0.5 0\npipe_stop=3 7 0.6 0\n"
+                 "pipe_stop=5 6 1.2 0\n")
+    marg, top = bench.ablation_marginals(str(p))
+    assert marg == {"k_pre": 0.1, "k_thr_ccl": 0.4, "k_ccl_merge": 0.1, "k_boundary": 0.6}
+    assert top == "k_boundary"

@@ -513,20 +513,72 @@ def test_ccl_merge_and_fallback_in_one_batch(gpu, oracle_mod):
         assert compare_detections(res[c], orc.detections()) == [], c
 
 
-def test_ccl_merge_counts_at_l2_1080p(gpu, oracle_mod):
-    """1080p noise frames list ~11 k local roots: more than the 14 B per root of pixel
-    counts fit beside the parent keys in k_ccl_merge's LDS, so the counts are summed in
-    the size plane at L2 (10 B per root) -- no frame may fall back to the global merge,
+def test_ccl_merge_lds_layouts_1080p(gpu, oracle_mod):
+    """k_ccl_merge's two LDS layouts at 1080p (153,600 B): a 1080p stream frame lists
+    ~11 k local roots, whose parent keys and pixel counts fit at 12 B per root; a frame
+    with more than 12,799 (and at most 15,360) listed roots keeps the counts in the size
+    plane at L2 (10 B per root).  Frames are a stream frame whose top rows are replaced
+    by a one-decimated-pixel checker band of growing height (every background pixel of
+    a tile border its own component); the band heights that land in the L2 range are
+    found by running each frame alone.  No frame may fall back to the global merge,
     and every stage (labels, sizes, kept bits) stays bit-exact against the oracle."""
     from ros_vision_amd import synth
-    frames = [synth.stream_frame(1920, 1080, k)[1] for k in (3, 7)]
+    base = synth.stream_frame(1920, 1080, 3)[1]
+    yy, xx = np.mgrid[0:1080, 0:1920]
+    chk = np.where(((xx // 2) + (yy // 2)) & 1, 230, 25).astype(np.uint8)
+    frames, roots = [], []
     det = gpu.GpuDetector(1920, 1080, max_batch=8)
-    res = det.detect_batch(frames, gpu.AT_FMT_GRAY8)
-    st = det.batch_stats()
-    assert st["ccl_fallback_frames"] == 0, st
-    assert st["ccl_listed_roots_max"] * 14 > 153600, st  # (the counts-at-L2 layout ran)
-    for c, f in enumerate(frames):
+    for rows in (0, 64, 128, 192, 256, 320, 384, 448):
+        f = base.copy()
+        f[:rows] = chk[:rows]
+        det.detect_batch([f], gpu.AT_FMT_GRAY8)
+        st = det.batch_stats()
+        frames.append(f)
+        roots.append(st["ccl_listed_roots_max"])
+        if st["ccl_listed_roots_max"] > 15360:
+            break
+    assert roots[0] * 12 + 4 <= 153600, roots  # the stream frame: counts in LDS
+    picked = [0] + [i for i, r in enumerate(roots) if 12 * r + 4 > 153600 and r <= 15360][:2]
+    assert len(picked) >= 2, roots  # (some band lands in the counts-at-L2 range)
+    res = det.detect_batch([frames[i] for i in picked], gpu.AT_FMT_GRAY8)
+    assert det.batch_stats()["ccl_fallback_frames"] == 0
+    for c, i in enumerate(picked):
         orc = oracle_mod.Oracle(1920, 1080)
-        orc.detect(f, 2)
-        assert compare_frame(det, orc, frame_idx=c) == [], c
-        assert compare_detections(res[c], orc.detections()) == [], c
+        orc.detect(frames[i], 2)
+        assert compare_frame(det, orc, frame_idx=c) == [], (c, roots[i])
+        assert compare_detections(res[c], orc.detections()) == [], (c, roots[i])
+
+
+def test_ccl_adversarial_unions(gpu, oracle_mod):
+    """k_thr_ccl runs no barrier between reading the union targets and
+    the unions, nor between the finds and the root writes (unions and compressions only
+    lower a parent within its component).  Frames built to race them (tests/ccl_patterns.py:
+    serpentine backgrounds between interleaved combs, spirals, staircases -- components
+    through every wave's block rows of a tile and across tile borders), at B = 1 (32-wide
+    tiles, k_ccl_border / k_ccl_roots) and B = 192 (64-wide tiles, k_ccl_merge): labels
+    (the component's minimum node id) and sizes bit-exact against the oracle for every
+    frame, every later stage for the first frames of each batch."""
+    import torch
+
+    import ccl_patterns
+    W, H, B = 1280, 720, 192
+    variants = [ccl_patterns.frame(W, H, seed) for seed in range(8)]
+    orcs = []
+    for f in variants:
+        o = oracle_mod.Oracle(W, H)
+        o.detect(f, 2)
+        orcs.append(o)
+    want = [(o.labels().copy(), o.sizes().copy()) for o in orcs]
+    det1 = gpu.GpuDetector(W, H)
+    for v in range(4):
+        det1.detect(variants[v], gpu.AT_FMT_GRAY8)
+        assert compare_frame(det1, orcs[v]) == [], v
+    batch = np.stack([variants[j % 8] for j in range(B)])
+    t = torch.from_numpy(batch).cuda()
+    det = gpu.GpuDetector(W, H, max_batch=B)
+    det.detect_device(t.data_ptr(), batch[0].nbytes, B, gpu.AT_FMT_GRAY8)
+    for j in range(B):
+        assert np.array_equal(det.copy_union_markers(j), want[j % 8][0]), j
+        assert np.array_equal(det.copy_union_markers_size(j), want[j % 8][1]), j
+    for j in range(8):
+        assert compare_frame(det, orcs[j], frame_idx=j) == [], j

@@ -15,9 +15,11 @@ import torch  # noqa: E402
 import ros_vision_amd as rva  # noqa: E402
 from ros_vision_amd import synth  # noqa: E402
 
-W, H = 1280, 720
+W, H = int(os.environ.get("LP_W", 1280)), int(os.environ.get("LP_H", 720))
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-frames = np.stack([synth.stream_frame(W, H, f)[0] for f in range(B)])
+NT = int(os.environ.get("LP_TAGS", 15))
+frames = np.stack([synth.stream_frame(W, H, f, ntags=NT)[0] for f in range(min(B, 16))])
+frames = frames[np.arange(B) % frames.shape[0]]
 d_frames = torch.from_numpy(frames).cuda()
 det = rva.GpuDetector(W, H, max_batch=B)
 for rep in range(3):
