@@ -154,6 +154,7 @@ struct at_detector {
   int last_nframes;
   int last_fmt;
   int last_gray;            // the last batch wrote the gray plane (AT_STAGE_GRAY)
+  int last_sizes;           // ... and the size plane (AT_STAGE_SIZES)
   int last_staged;          // the last batch's frames were host frames staged in d_in (at_detect*)
   int last_gp;              // the last batch ran the game-piece preprocessing (k_gp_pre)
   int pending;
@@ -721,6 +722,7 @@ static int enqueue(at_detector* d, int nframes, int fmt) {
   d->last_nframes = nframes;
   d->last_fmt = fmt;
   d->last_gray = fmt == AT_FMT_BGR8 || d->prm.taps;  // (YUYV / GRAY8: k_decode samples the frame)
+  d->last_sizes = d->g.ctw == 32 || d->prm.taps;     // (throughput mode: the size plane for the taps only)
   d->last_gp = d->prm.gp_c && fmt == AT_FMT_BGR8;
   d->pending = 1;
   return AT_OK;
@@ -1224,7 +1226,7 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
     }
     case AT_STAGE_SIZES: {
       // the dense plane of the reference, masked from the forest on the device
-      if (bytes < nd * 4) return AT_E_INVALID;
+      if (bytes < nd * 4 || !d->last_sizes) return AT_E_INVALID;
       uint32_t* tmp_d = nullptr;
       if (hipMalloc(&tmp_d, nd * 4) != hipSuccess) return AT_E_NOMEM;
       hipError_t e = launch_tap_sizes(d->d.thr + frame * nd, d->d.par + frame * nd, d->d.size + frame * nd, tmp_d,

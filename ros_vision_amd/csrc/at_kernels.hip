@@ -908,11 +908,18 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     };
     *reinterpret_cast<uint2*>(par + idF) = make_uint2(word(rF, wF, cF, lF, iF), idF + 1);
     *reinterpret_cast<uint2*>(par + idL) = make_uint2(word(rL, wL, cL, lL, iL), word(rR, wR, cR, lR, iR));
-    if (cF) size[idF] = cF;
-    if (cL | cR) {
-      if (cL && cR) *reinterpret_cast<uint2*>(size + idL) = make_uint2(cL, cR);
-      else if (cL) size[idL] = cL;
-      else size[idL + 1] = cR;
+    // local counts at local roots: latency mode sums them at the component roots
+    // (k_ccl_roots) and k_boundary tests them; throughput mode carries the kept bit
+    // in the root words instead (and k_ccl_merge the counts in its lists), so the
+    // plane is written only for the AT_STAGE_SIZES tap -- ~12 k scattered 4-B stores
+    // per 720p frame (0.3 MB of write traffic) otherwise
+    if (!kKeep || prm.taps) {
+      if (cF) size[idF] = cF;
+      if (cL | cR) {
+        if (cL && cR) *reinterpret_cast<uint2*>(size + idL) = make_uint2(cL, cR);
+        else if (cL) size[idL] = cL;
+        else size[idL + 1] = cR;
+      }
     }
   }
   if constexpr (TWD == 64) {
@@ -1239,11 +1246,12 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
     // global memory by this workgroup -- k_ccl_border's unions (atomicMin links on the
     // parent words), then k_ccl_roots' pass and the kept bits over the lists.  Slow
     // (one workgroup for the frame) but rare; the frame's result is the same.
-    for (int t = tid >> 6; t < ntl; t += 16) {  // plain root words back first
+    for (int t = tid >> 6; t < ntl; t += 16) {  // plain root words and local counts back first
       const uint32_t n = s_base[t + 1] - s_base[t];
       for (uint32_t k = lane_id(); k < n; k += 64) {
         const uint32_t l = lroot[(size_t)t * kCclTileNodesMax + k];
         par[l] = l;
+        size[l] = lcnt_of(b, f, ntl, t, k);  // (k_thr_ccl writes the plane for the taps only)
       }
     }
     if (tid == 0) b.ccl_ovf[f] = 1u;
@@ -1306,8 +1314,10 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
         const size_t e = (size_t)t * kCclTileNodesMax + (i - s_base[t]);
         mg[j] = lroot[e];
         s_key[i] = ((uint64_t)mg[j] << 32) | i;
+        size[mg[j]] = lcnt[e];  // the root's own count, summed into below (counts at L2)
       }
     }
+    __threadfence();  // (those stores at L2 before any lane's atomicAdd to them)
   }
   __syncthreads();
   stamp(2);
@@ -1454,7 +1464,7 @@ __global__ __launch_bounds__(1024) void k_ccl_merge(DevBufs b, Geom g, Params pr
         const uint32_t root = (uint32_t)(key_load(s_key + r) >> 32);
         const uint32_t cnt = s_cnt[r];
         par[node] = root | (cnt >= 25 ? kKeptBit : 0u);
-        if (r == i) size[node] = cnt;
+        if (prm.taps && r == i) size[node] = cnt;  // (the AT_STAGE_SIZES tap)
       }
     }
   } else {
@@ -3378,6 +3388,7 @@ __device__ __forceinline__ PairInfo load_pair_info(const DevBufs& b, uint32_t w)
   return PairInfo{b.pair_cnt[i], b.pair_off[i], b.pair_sel[i]};
 }
 
+
 template <int NT, int CAP, bool FUSE = false>
 __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, BlobShared<NT, CAP>& S, uint64_t* gpk,
                           const uint32_t* combo, uint32_t w, PairInfo pi_, uint32_t* pacc) {
@@ -3941,6 +3952,9 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 #ifndef AT_EXT_KEY_UNROLL
 #define AT_EXT_KEY_UNROLL 4
 #endif
+#ifndef AT_EXT_KR
+#define AT_EXT_KR 1  // the first round's grouped points kept in registers for the key pass
+#endif
   uint32_t kr[U];
   for (uint32_t base = 0; base < n; base += NT * U) {
     uint32_t kk[U];
@@ -3951,7 +3965,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      if (base == 0) kr[u] = kk[u];
+      if (AT_EXT_KR && base == 0) kr[u] = kk[u];
       if (base + u * NT + tid >= n) continue;
       const uint64_t k = kk[u];
       const int dxy = (int)(k & 3);
@@ -4000,7 +4014,7 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t t = base + u * NT + tid;
-      kk[u] = base == 0 ? kr[u] : (t < n ? grp[t] : 0);
+      kk[u] = (AT_EXT_KR && base == 0) ? kr[u] : (t < n ? grp[t] : 0);
     }
     // line-fit weight of TransformLineFitPoint (apriltag_gpu.cu:631-687): gradient
     // of the decimated image at ((px + 1) / 2, (py + 1) / 2); the four bytes of
@@ -4046,11 +4060,12 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
 
 // Large candidates (size classes 0-2) one per workgroup, then small ones one
 // per wave.
-// 6 waves per SIMD (80 VGPRs with 4 points per lane in flight) and a grid that fills
-// them: k_extents 0.152 -> 0.131 ms per 128 frames against 4 waves / 8 points per lane
-// (127 VGPRs), concurrent throughput unchanged or better (profiles/r04n, r04o)
+// 4 points per lane in flight and a grid of 1536 persistent workgroups: at 6 waves per
+// SIMD (80 VGPRs) k_extents took 0.131 ms per 128 frames against 0.152 at 4 waves / 8
+// points per lane (profiles/r04n, r04o); at 5 (below) it runs without spills.
 #ifndef AT_EXT_WAVES
-#define AT_EXT_WAVES 6
+#define AT_EXT_WAVES 5  // 6 (80 VGPRs) spilled 10 VGPRs since det_atan2's one-division form: +0.35 MB of
+                        // scratch traffic per frame (profiles/r06/pmc_ext_ab.txt); 93 VGPRs fit 5
 #endif
 #ifndef AT_EXT_GRID
 #define AT_EXT_GRID 1536  // workgroups (persistent over the candidates): AT_EXT_WAVES x 256 CUs / 4

@@ -11,6 +11,7 @@
 #   BENCH=1            the default bench line -> bench.json
 #   LIBS="a.so b.so"   interleaved concurrent A/B at 720p (tools/ab_stages.sh)
 #   LIBS1080="a b"     the same at 1080p
+#   PMCLIBS="a b"      FETCH / WRITE bytes per kernel of each library (tools/pmc_ab.sh)
 #   ISO=1              bench.py --isolated-only under rocprofv3 --kernel-trace --stats
 set -o pipefail
 TAG=${TAG:-r06}; O=gpurun_out/$TAG; mkdir -p $O
@@ -54,6 +55,7 @@ if [ -n "${LIBS1080:-}" ]; then
 import json,sys; j=json.load(sys.stdin); print(j['value'], j['detections_per_frame'], ' '.join('%s=%.4f' % kv for kv in j['stage_ms_per_batch'].items()))" >> $O/ab1080.txt || exit 1
   done; done
 fi
+if [ -n "${PMCLIBS:-}" ]; then LIBS="$PMCLIBS" TAG=$TAG/pmc bash tools/pmc_ab.sh > $O/pmc_ab.txt 2> $O/pmc_ab.err || exit 1; fi
 if [ -n "${ISO:-}" ]; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/trace_iso -o run -- \
      python3 $R/bench.py --isolated-only > $R/$O/iso_traced.json 2> $R/$O/iso_traced.err) || exit 1
