@@ -1294,17 +1294,30 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       if (hipMemcpy(ekey.data(), d->d.pent_key + frame * ntb * kLdsPairSlots, ekey.size() * 8,
                     hipMemcpyDeviceToHost) != hipSuccess)
         return AT_E_HIP;
+      // the device keys pairs by node index (node_F / node_L: three words per 2x2 block,
+      // monotone in the node id); the reference's QuadBoundaryPoint carries the node ids
+      auto node_id = [&](uint64_t n) -> uint64_t {
+        const uint64_t P = 3 * (uint64_t)g.BW, by = n / P, r = n - by * P;
+        return r < (uint64_t)g.BW ? 2 * by * g.Wd + 2 * r : (2 * by + 1) * g.Wd + (r - g.BW);
+      };
+      auto to_ref = [&](uint64_t k) -> uint64_t {
+        return (node_id(k >> 44) << 44) | (node_id((k >> 24) & 0xfffff) << 24) | (k & 0xffffffu);
+      };
       size_t o = 0;
       for (size_t t = 0; t < ntb; t++) {
         const uint32_t n = tc[t] & ~kTileNarrow;
         if (tc[t] & kTileNarrow) {
           const uint32_t* w = reinterpret_cast<const uint32_t*>(all.data() + t * g.bnd_region);
           for (uint32_t i = 0; i < n; i++) {
-            const uint64_t key = (ekey[t * kLdsPairSlots + (w[i] >> 23)] << 24) | ((w[i] & 0x7ffffcu) << 1) | (w[i] & 3u);
+            const uint64_t key =
+                to_ref((ekey[t * kLdsPairSlots + (w[i] >> 23)] << 24) | ((w[i] & 0x7ffffcu) << 1) | (w[i] & 3u));
             memcpy((uint8_t*)dst + (o + i) * 8, &key, 8);
           }
         } else {
-          memcpy((uint8_t*)dst + o * 8, all.data() + t * g.bnd_region, (size_t)n * 8);
+          for (uint32_t i = 0; i < n; i++) {
+            const uint64_t key = to_ref(all[t * g.bnd_region + i]);
+            memcpy((uint8_t*)dst + (o + i) * 8, &key, 8);
+          }
         }
         o += n;
       }

@@ -375,6 +375,21 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g, int wgray) {
 // ---------------------------------------------------------------------------
 // (relaxed atomic loads, not volatile: a volatile access through the generic
 // pointer would be compiled to flat instructions instead of ds_read)
+// Union-find node index (the parent plane, the size plane, the labels the later stages
+// key pairs by): the nodes of 2x2-block row BY are stored contiguously, its BW fg nodes
+// (F, the block's top-left pixel) then its 2 BW bg nodes (L, R: bottom-left, bottom-right)
+// -- 3 words per block instead of one per pixel (the top-right pixel is no node).  The
+// index is monotone in the reference's node id (the pixel index), so a component's
+// minimum index is its minimum node id, the reference's label (node_pixel maps back).
+__device__ __forceinline__ uint32_t node_F(const Geom& g, int BY, int BX) { return (uint32_t)(BY * 3 * g.BW + BX); }
+__device__ __forceinline__ uint32_t node_L(const Geom& g, int BY, int BX) {
+  return (uint32_t)(BY * 3 * g.BW + g.BW + 2 * BX);
+}
+__device__ __forceinline__ uint32_t node_pixel(int BW, int Wd, uint32_t n) {
+  const uint32_t by = n / (uint32_t)(3 * BW), r = n - by * (uint32_t)(3 * BW);
+  return r < (uint32_t)BW ? 2 * by * (uint32_t)Wd + 2 * r : (2 * by + 1) * (uint32_t)Wd + (r - (uint32_t)BW);
+}
+
 __device__ __forceinline__ uint32_t lds_load(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -828,7 +843,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
   ph(7);
   // every slot's global node id, by its owner (the publish looks its roots' ids up
   // instead of decoding slot numbers: ~15 VALU per decode)
-  const uint32_t idF = (uint32_t)(2 * (y0 / 2 + bty) * g.Wd + 2 * (x0 / 2 + btx)), idL = idF + g.Wd;
+  const uint32_t idF = node_F(g, y0 / 2 + bty, x0 / 2 + btx), idL = node_L(g, y0 / 2 + bty, x0 / 2 + btx);
   s_gid[F] = idF;
   s_gid[L] = idL;
   s_gid[R] = idL + 1;
@@ -906,7 +921,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     auto word = [&](uint32_t r, uint32_t w, uint32_t c, bool listed, uint32_t li) -> uint32_t {
       return (kKeep && listed) ? kListBit | li : gid(r) | fin(w, c);
     };
-    *reinterpret_cast<uint2*>(par + idF) = make_uint2(word(rF, wF, cF, lF, iF), idF + 1);
+    par[idF] = word(rF, wF, cF, lF, iF);
     *reinterpret_cast<uint2*>(par + idL) = make_uint2(word(rL, wL, cL, lL, iL), word(rR, wR, cR, lR, iR));
     // local counts at local roots: latency mode sums them at the component roots
     // (k_ccl_roots) and k_boundary tests them; throughput mode carries the kept bit
@@ -1066,29 +1081,32 @@ __device__ __forceinline__ void border_candidate(const DevBufs& b, const Geom& g
   };
   const bool act = role != 3;  // (no loads outside the image for the padding threads)
   const uint8_t a = act ? thr[idx] : 127, bb = act ? thr[idx + 1] : 127, c = act ? thr[idx + Wd] : 127;
-  const uint32_t F = (uint32_t)idx, L = (uint32_t)(idx + Wd), R = L + 1;
+  // nodes of this block and of its neighbours: F -/+ 1 (left / right), -/+ P (block row
+  // above / below), L - 1 = the left block's R
+  const uint32_t P = 3 * (uint32_t)g.BW;
+  const uint32_t F = node_F(g, BY, BX), L = node_L(g, BY, BX), R = L + 1;
   uint32_t u = 0, v = 0;
   bool link = false;
   if (role == 0 && BY > 0) {
-    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    if (kind == 0) { link = a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - P - 1; }
     else if (kind == 1) {
       link = (a == 255 || bb == 255) && (px(row - 1, col) == 255 || px(row - 1, col + 1) == 255);
-      u = F; v = F - 2 * Wd;
+      u = F; v = F - P;
     }
-    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2; }
-    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - 2 * Wd; }
-    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - 2 * Wd; }
+    else if (kind == 2) { link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - P + 1; }
+    else if (kind == 3) { link = a == 0 && px(row - 1, col) == 0; u = L; v = L - P; }
+    else { link = bb == 0 && px(row - 1, col + 1) == 0; u = R; v = R - P; }
   } else if (role == 1 && BX > 0) {
-    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - 2 * Wd - 2; }
+    if (kind == 0) { link = BY > 0 && bty > 0 && a == 255 && px(row - 1, col - 1) == 255; u = F; v = F - P - 1; }
     else if (kind == 1) {
       link = (a == 255 || c == 255) && (px(row, col - 1) == 255 || px(row + 1, col - 1) == 255);
-      u = F; v = F - 2;
+      u = F; v = F - 1;
     } else {
       link = (a == 0 && px(row, col - 1) == 0) || (c == 0 && px(row + 1, col - 1) == 0);
       u = L; v = L - 1;
     }
   } else if (role == 2 && BY > 0) {
-    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - 2 * Wd + 2;
+    link = bb == 255 && px(row - 1, col + 2) == 255; u = F; v = F - P + 1;
   }
   if (link) g_union2(par, u, v);
 }
@@ -1637,9 +1655,9 @@ __global__ __launch_bounds__(256) AT_BND_ATTR void k_boundary(DevBufs b, Geom g)
     const int yy = ty0 + ec / kTC, xx = tx0 + ec % kTC;
     const bool in = e < kTN && yy < g.Hd && xx < Wd;
     const int yc = min(yy, g.Hd - 1), xc = min(xx, Wd - 1);
-    const uint32_t F = (uint32_t)((yc & ~1) * Wd + (xc & ~1));
+    const uint32_t F = node_F(g, yc >> 1, xc >> 1), LR = node_L(g, yc >> 1, 0) + (uint32_t)xc;
     const uint8_t t = thr[(size_t)yc * Wd + xc];
-    const uint32_t a = par[F], c = par[F + Wd + (xc & 1)];
+    const uint32_t a = par[F], c = par[LR];
     tv[k] = in ? t : (uint8_t)127;
     lv[k] = in ? a : 0xffffffffu;
     lb[k] = in ? c : 0xffffffffu;
@@ -2189,14 +2207,20 @@ __global__ __launch_bounds__(1024) void k_pairs(DevBufs b, Geom g, int probe) {
 // count word now holds the base, kGrpDrop for pairs outside SelectBlobs' count
 // bounds -- P4's size filter: nothing reads their segments); the tile's points
 // take consecutive slots of their entry's range (LDS cursor).  The tile's
-// counters, its entries and its first 1024 points are loaded in ONE round trip
+// counters, its entries and its first 512 points are loaded in ONE round trip
 // (speculatively: reads past the counts stay inside the tile's regions).  Points
 // of later entries (crowded tiles) and of pairs missing from the tile's entries
 // (LDS table overflow in k_boundary) reserve one slot each.
-// loaded up front, before the tile's counts are known: the first 512 points and
-// 32 entries (typical tiles: ~670 points, ~10 entries), so the speculation reads
-// little past the counts; the rest of a crowded tile follows once they are known
-constexpr int kGrpPre = 2;
+// loaded up front, before the tile's counts are known: the first 256 8-B keys or 512
+// narrow words and 32 entries (typical tiles: ~700 narrow points, ~10 entries), so the
+// speculation reads nothing past the counts of most tiles; the rest follows once they
+// are known.  (1024 narrow words up front read ~1.2 KB past a typical tile's points:
+// 11.08 -> 10.83 MB per frame with half of that, concurrent throughput unchanged,
+// profiles/r06/pmc_grp_pre_ab.txt)
+#ifndef AT_GRP_PRE
+#define AT_GRP_PRE 1
+#endif
+constexpr int kGrpPre = AT_GRP_PRE;
 constexpr int kGrpEntPre = 32;
 __global__ __launch_bounds__(256) void k_group(DevBufs b, Geom g) {
   const TileIdx bi = xcd_block<AT_XCD_GRP>();
@@ -4915,15 +4939,19 @@ __global__ __launch_bounds__(256) void k_tap_sizes(const uint8_t* thr, const uin
   if (i >= Wd * Hd) return;
   const int y = i / Wd, x = i % Wd;
   const int F = (y & ~1) * Wd + (x & ~1);
+  const int BW = Wd / 2;
   uint32_t v = 0;
   bool node = true, has = false;
+  uint32_t n = 0;  // the node's index (node_F / node_L)
   if ((y & 1) == 0) {
     if (x & 1) node = false;  // (2r, 2c+1) is not a node
     else has = thr[F] == 255 || thr[F + 1] == 255 || (y + 1 < Hd && (thr[F + Wd] == 255 || thr[F + Wd + 1] == 255));
+    n = (uint32_t)((y >> 1) * 3 * BW + (x >> 1));
   } else {
     has = thr[i] == 0 || thr[i - Wd] == 0;  // the block's column of this bg node
+    n = (uint32_t)((y >> 1) * 3 * BW + BW + x);
   }
-  if (node && has && (par[i] & ~kKeptBit) == (uint32_t)i) v = size[i];
+  if (node && has && (par[n] & ~kKeptBit) == n) v = size[n];
   out[i] = v;
 }
 
@@ -4941,7 +4969,11 @@ __global__ __launch_bounds__(256) void k_tap_labels(const uint8_t* thr, const ui
   uint32_t lab;
   if (all127) lab = (uint32_t)i;
   else if (thr[i] == 127) lab = 0;
-  else lab = par[par[thr[i] == 255 ? F : F + Wd + (x & 1)] & ~kKeptBit] & ~kKeptBit;
+  else {
+    const int BW = Wd / 2;
+    const uint32_t n = thr[i] == 255 ? (uint32_t)((y >> 1) * 3 * BW + (x >> 1)) : (uint32_t)((y >> 1) * 3 * BW + BW + x);
+    lab = node_pixel(BW, Wd, par[par[n] & ~kKeptBit] & ~kKeptBit);
+  }
   out[i] = lab;
 }
 
