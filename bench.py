@@ -40,7 +40,7 @@ METRIC = "frames/sec + p50 per-frame latency, 1280x720 AprilTag detect at 1/2/4/
 # tools/r06_call.sh ABL=1), re-derived at HEAD and committed as ABLATION; every line
 # reports that file's marginal costs and flags a DOMINANT that no longer matches it
 # (tests/test_bench_cli.py checks the pair).
-DOMINANT = "k_thr_ccl"
+DOMINANT = "k_boundary"
 ABLATION = "profiles/r06/ablation_720p.txt"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -142,8 +142,9 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_pre":
         return nf * (2 * W * H + W * H + Wd * Hd)           # YUYV in, gray + decimated out
     if kernel == "k_boundary":
-        # thr + labels in; points out as the 4-B (pair entry, point bits) words of narrow tiles
-        return nf * 5 * Wd * Hd + 4 * stats.get("boundary_points", 0)
+        # thr (1 B per decimated pixel) + the parent words (3 words per 2x2 block: 3 B per
+        # pixel) in; points out as the 4-B (pair entry, point bits) words of narrow tiles
+        return nf * 4 * Wd * Hd + 4 * stats.get("boundary_points", 0)
     if kernel == "k_blob":  # kept blobs: the 8-B sort key of every point (the line-fit weight W rides in it)
         return 8 * stats.get("large_blob_points", 0)
     if kernel == "k_blob_small":
@@ -151,9 +152,9 @@ def kernel_algorithmic_bytes(kernel, stats, W, H):
     if kernel == "k_extents":  # candidate points read (bounded by all boundary points), kept points' keys written
         return 8 * stats.get("boundary_points", 0) + 8 * (stats.get("small_blob_points", 0) +
                                                           stats.get("large_blob_points", 0))
-    if kernel == "k_thr_ccl":  # dec in; thr and parent words out; lists (id, count) and border descriptors out
+    if kernel == "k_thr_ccl":  # dec in; thr and parent words (3 per 2x2 block) out; lists (id, count), descriptors out
         tiles = ((Wd + 63) // 64) * ((Hd + 31) // 32)
-        return nf * 6 * Wd * Hd + 8 * stats.get("ccl_listed_roots", 0) + nf * tiles * 704
+        return nf * 5 * Wd * Hd + 8 * stats.get("ccl_listed_roots", 0) + nf * tiles * 704
     if kernel == "k_ccl_border":  # per 32x32 tile: 47 border blocks, thr bytes + parent words
         return nf * ((Wd + 31) // 32) * ((Hd + 31) // 32) * 47 * 16
     if kernel == "k_ccl_merge":  # border descriptors (704 B per 64x32 tile) + listed roots (id, count) in, words out
