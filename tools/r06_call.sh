@@ -9,6 +9,7 @@
 #   P1080=1            1080p profile: bench line with stage profile + isolated kernels,
 #                      FETCH / WRITE passes (pmc_traffic_1080p.json)
 #   BENCH=1            the default bench line -> bench.json
+#   BSTOPS="0 2 3 4 7 8"  blob kernels cut after a phase (experiment build): serialized stage ms
 #   LIBS="a.so b.so"   interleaved concurrent A/B at 720p (tools/ab_stages.sh)
 #   LIBS1080="a b"     the same at 1080p
 #   PMCLIBS="a b"      FETCH / WRITE bytes per kernel of each library (tools/pmc_ab.sh)
@@ -45,6 +46,14 @@ if [ -n "${P1080:-}" ]; then
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$O/pmc1080_fetch -o run -- python3 $SHORT > /dev/null 2> $R/$O/pmc1080_fetch.err) || exit 1
   (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$O/pmc1080_write -o run -- python3 $SHORT > /dev/null 2> $R/$O/pmc1080_write.err) || exit 1
   python3 tools/pmc_traffic.py $O/pmc1080_fetch/run_counter_collection.csv $O/pmc1080_write/run_counter_collection.csv 192 1920 1080 $O/pmc_traffic_1080p.json > /dev/null || exit 1
+fi
+if [ -n "${BSTOPS:-}" ]; then  # blob kernels cut after phase N (AT_DIAG_BLOB_STOP): serialized stage times
+  for r in 1 2; do for st in $BSTOPS; do
+    echo -n "round=$r blob_stop=$st " >> $O/blob_stops.txt
+    AT_HIP_LIB=$EXP AT_DIAG_BLOB_STOP=$st timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --latency-frames 0 \
+      --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --no-kernel-timer 2>>$O/err.txt | python3 -c "
+import json,sys; j=json.load(sys.stdin); s=j['stage_ms_per_batch']; print(j['value'], 'k_blob_small=%.4f k_blob=%.4f k_decode=%.4f' % (s['k_blob_small'], s['k_blob'], s['k_decode']))" >> $O/blob_stops.txt || exit 1
+  done; done
 fi
 if [ -n "${LIBS:-}" ]; then TAG=$TAG bash tools/ab_stages.sh > /dev/null || exit 1; fi
 if [ -n "${LIBS1080:-}" ]; then
