@@ -453,6 +453,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.dets = (DevDetection*)dalloc(B * kMaxDets * sizeof(DevDetection));
   b.det_work = (uint32_t*)dalloc(B * kMaxDets * 4);
   b.quads = (QuadRecord*)dalloc(B * kMaxPairs * sizeof(QuadRecord));
+  b.qpend = (QuadPend*)dalloc(B * kMaxPairs * sizeof(QuadPend));
   // control block: per-frame words, scalars, then (8-byte aligned) the timed
   // kernel's two wall-clock stamps and its finished-workgroup count
   d->kstamp_word = (kCtlPerFrame * B + kCtlScalars + 1) & ~(size_t)1;
@@ -464,7 +465,8 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   b.nquads = d->d_ctrl + kCtlNquads * B;
   b.status = d->d_ctrl + kCtlStatus * B;
   b.npent = d->d_ctrl + kCtlNpent * B;
-  b.nqcand = d->d_ctrl + kCtlNqcand * B;
+  b.qc_words = (uint32_t)(B * kQcStride);
+  b.nqcand = (uint32_t*)dalloc((size_t)b.qc_words * 4);
   b.ccl_ovf = d->d_ctrl + kCtlCclOvf * B;
   b.nlr_tot = d->d_ctrl + kCtlNlr * B;
   uint32_t* sc = d->d_ctrl + kCtlPerFrame * B;

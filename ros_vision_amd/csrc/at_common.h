@@ -101,6 +101,7 @@ constexpr int kMaxBatch = 256;          // frames per launch sequence (at_config
 // Every kept blob pair can yield one accepted quad and every accepted quad at most
 // one detection, so sizing both queues by kMaxPairs makes neither of them a cap:
 // the reference decodes every quad (apriltag_detect.cu:618-663).
+constexpr int kQcStride = 32;  // words between two frames' accepted-quad counters (DevBufs::nqcand)
 constexpr int kQuadCandPerFrame = kMaxPairs;  // accepted quads queued for decode, per frame
 constexpr int kMaxDets = kQuadCandPerFrame;   // candidate detections one frame can have (before reconcile)
 // Candidate detections: every frame owns kMaxDets records in HBM (frame f's k-th
@@ -170,10 +171,12 @@ constexpr int kProbeWords = 256;
 #define AT_DIAG_STOP(prm, n) ((prm).diag_stop == (n))
 #define AT_PIPE_STOP(prm) ((prm).pipe_stop)
 #define AT_PROBE_ON(prm) ((prm).probe != 0)
+#define AT_DIAG_ANY(prm) ((prm).diag_stop != 0)
 #else
 #define AT_DIAG_STOP(prm, n) false
 #define AT_PIPE_STOP(prm) 0
 #define AT_PROBE_ON(prm) false
+#define AT_DIAG_ANY(prm) false
 #endif
 
 // HIP events bracketing one kernel of the launch sequence (bench roofline).
@@ -215,6 +218,24 @@ struct QuadRecord {
   uint32_t blob_index, valid, accepted;
   uint16_t indices[4];
   float corners[4][2];
+};
+
+// Moments of a run of line-fit points in the reference's widths (LineFitPoint sums,
+// line_fit_filter.h:61-83), with the run's point count.
+struct Moments {
+  int32_t Mx, My, W;
+  int64_t Mxx, Myy, Mxy;
+  int32_t N;
+};
+
+// A kept blob's side fits left to k_quad_fin (throughput mode): the moments of the
+// four side segments of its best combination, and the record's fields.  The blob's
+// wave writes them (lanes 0-3 a segment each); k_quad_fin fits the four lines, the
+// corners and the Heron / angle tests with a thread per blob.
+struct QuadPend {
+  Moments seg[4];
+  uint32_t blob_index, valid;
+  uint16_t indices[4];
 };
 
 // One 2-px-thick segment of the annotated image (at_draw_outlines_device).
@@ -274,6 +295,7 @@ struct DevBufs {
   uint32_t* ctrl;       // device control block base
   uint32_t ctrl_words;
   QuadRecord* quads;  // [B][kMaxPairs]  fitted-quad debug record of each kept blob, slot = pair rank
+  QuadPend* qpend;    // [B][kMaxPairs]  side-fit inputs of each kept blob (throughput mode), slot = pair rank
   // control block (zeroed every batch)
   uint32_t* npts;     // [B]
   uint32_t* npairs;   // [B]
@@ -286,7 +308,10 @@ struct DevBufs {
   uint32_t* blob_pts;       // [2] points processed by the small / large blob kernels (batch statistics)
   uint32_t* workhead_small; // [1] dequeue head of the stage's second large-blob launch
   uint32_t* workhead_mid;   // [1] ... and of its third
-  uint32_t* nqcand;   // [B] accepted quads queued for decode, per frame (qcand[f][kQuadCandPerFrame])
+  uint32_t* nqcand;   // [B][kQcStride] accepted quads queued for decode, per frame (qcand[f][kQuadCandPerFrame]):
+                      //     a 128-B line per frame, so one frame's appends never wait behind another's
+                      //     (zeroed with the control block, by the first kernel's block 0)
+  uint32_t qc_words;  // B * kQcStride
   uint32_t* qhead;    // [1]
   QuadCand* qcand;    // [qcand_cap]
   uint32_t qcand_cap;

@@ -332,8 +332,10 @@ __global__ __launch_bounds__(256) void k_pre(DevBufs b, Geom g, int wgray) {
   const int ty = bi.y * 4 + threadIdx.y;
   // the batch's control block starts at zero (no memset node): nothing in k_pre
   // reads it, every later kernel follows in stream order
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
     for (uint32_t w = threadIdx.y * 64 + threadIdx.x; w < b.ctrl_words; w += 256) b.ctrl[w] = 0;
+    for (uint32_t w = threadIdx.y * 64 + threadIdx.x; w < b.qc_words; w += 256) b.nqcand[w] = 0;
+  }
   if (tx >= g.TW || ty >= g.TH) return;
   const uint8_t* in = b.frames[f];
   uint8_t* gray = b.gray + (size_t)f * g.W * g.H;
@@ -505,6 +507,7 @@ __device__ __forceinline__ void thr_ccl_tile(const DevBufs& b, const Geom& g, co
     // reads it, every later kernel follows in stream order
     if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
       for (uint32_t w = tid; w < b.ctrl_words; w += NT) b.ctrl[w] = 0;
+      for (uint32_t w = tid; w < b.qc_words; w += NT) b.nqcand[w] = 0;
       __syncthreads();
     }
   }
@@ -2394,12 +2397,6 @@ __device__ __forceinline__ int32_t lf_weight(int32_t gx, int32_t gy) {
   return (int32_t)r + 1;
 }
 
-struct Moments {
-  int32_t Mx, My, W;
-  int64_t Mxx, Myy, Mxy;
-  int32_t N;
-};
-
 // FitLine (line_fit_filter.cu:798-872) / HostFitLine (apriltag_detect.cu:38-90)
 __device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* err, double* mse) {
   const int64_t W = m.W;
@@ -3812,6 +3809,21 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
   uint16_t qidx[4];
   const uint32_t cbt = combo[bt];
   for (int k = 0; k < 4; k++) qidx[k] = (uint16_t)S.pi[(cbt >> (8 * k)) & 0xff];
+  if constexpr (!FUSE) {
+    // throughput mode: the side segments' moments for k_quad_fin (a thread per blob
+    // there, instead of a few lanes of this team on a serial fp64 chain here)
+    QuadPend& qp = b.qpend[(size_t)f * kMaxPairs + rank];
+    if (valid && tid < 4) qp.seg[tid] = seg_moments((cbt >> (8 * tid)) & 0xff, (cbt >> (8 * ((tid + 1) & 3))) & 0xff);
+    if (tid == 0) {
+      qp.blob_index = bi;
+      qp.valid = valid;
+      for (int k = 0; k < 4; k++) qp.indices[k] = qidx[k];
+      pacc[21] += 1;  // FitQuads records of this team (batch statistics)
+    }
+    phase(9);
+    team_sync<NT>();
+    return;
+  }
   // UpdateFitQuads (apriltag_detect.cu:98-241): side lines in parallel, rest on one lane
   if (valid && tid < 4) {
     const LineFitOut o =
@@ -3904,7 +3916,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     if (ok && !AT_DIAG_STOP(prm, 5)) {
       qcand.frame = (uint32_t)f;
       qcand.rank = rank;
-      const uint32_t ci = atomicAdd(b.nqcand + f, 1u);  // per-frame counters spread the contention
+      const uint32_t ci = atomicAdd(b.nqcand + (size_t)f * kQcStride, 1u);  // per-frame counters spread the contention
       if (ci < (uint32_t)kQuadCandPerFrame) b.qcand[(size_t)f * kQuadCandPerFrame + ci] = qcand;
       else atomicOr(b.status + f, kStatusQuadsOverflow);
     }
@@ -4317,6 +4329,123 @@ __global__ __launch_bounds__(512) void k_blob_lat(DevBufs b, Geom g, Params prm)
   }
 }
 
+// Throughput mode's end of FitQuads (UpdateFitQuads, apriltag_detect.cu:98-241) for the
+// kept blobs of size classes c0 .. c1-1, four lanes (a DPP quad) per blob: lane k fits
+// side line k from the moments the blob kernels left in QuadPend, intersects it with
+// line k+1 (corner k), measures Heron side k (lanes 0, 1 also sides 4, 5) and tests
+// corner angle k; lane 0 writes the debug record and the accepted quad's decode-queue
+// entry.  The expressions are the team version's in blob_item (which latency mode keeps).
+__global__ __launch_bounds__(256) void k_quad_fin(DevBufs b, Geom g, Params prm, int c0, int c1) {
+  __shared__ uint32_t s_cnt[kNumCls];
+  if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
+  __syncthreads();
+  uint32_t nwork = 0;
+  for (int c = c0; c < c1; c++) nwork += s_cnt[c];
+  const uint32_t lane = lane_id(), base = lane & ~3u;
+  const int k = (int)(lane & 3);
+  auto from = [&](double v, int j) { return __shfl(v, (int)base + j); };
+  auto fromf = [&](float v, int j) { return __shfl(v, (int)base + j); };
+  auto quad_or = [&](int v) {
+    v |= __shfl_xor(v, 1);
+    return v | __shfl_xor(v, 2);
+  };
+  // (the four lanes of a quad share the item: every shuffle reads an active lane)
+  for (uint32_t it = (blockIdx.x * 256 + threadIdx.x) >> 2; it < nwork; it += gridDim.x * 64) {
+    uint32_t w = 0;
+    work_item(b, s_cnt, c0, c1, it, &w);
+    const uint32_t f = w >> 16, rank = w & 0xffff;
+    const size_t slot = (size_t)f * kMaxPairs + rank;
+    if (b.pair_sel[slot] == 0) continue;  // (the blob kernels skipped it too)
+    const QuadPend& qp = b.qpend[slot];
+    const bool valid = qp.valid != 0;
+    float cx = 0.f, cy = 0.f;
+    int bad = 0;
+    {
+      double l[4] = {0, 0, 0, 0};
+      if (valid) {
+        const LineFitOut o = fit_line_v<true, true>(qp.seg[k]);
+        l[0] = o.p01[0]; l[1] = o.p01[1]; l[2] = o.p23[0]; l[3] = o.p23[1];
+      }
+      double m[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) m[j] = from(l[j], (k + 1) & 3);  // line k+1
+      if (valid) {
+        const double A00 = l[3], A01 = -m[3];
+        const double A10 = -l[2], A11 = m[2];
+        const double B0 = -l[0] + m[0];
+        const double B1 = -l[1] + m[1];
+        const double det = A00 * A11 - A10 * A01;
+        const double W00 = A11 / det, W01 = -A01 / det;
+        if (fabs(det) < 0.001) {
+          bad = 1;
+        } else {
+          const double L0 = W00 * B0 + W01 * B1;
+          cx = (float)(l[0] + L0 * A00);
+          cy = (float)(l[1] + L0 * A10);
+        }
+      }
+    }
+    bool ok = valid && !quad_or(bad);
+    float qc[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      qc[j][0] = fromf(cx, j);
+      qc[j][1] = fromf(cy, j);
+    }
+    if (ok) {
+      // sides of triangles (0,1,2) and (2,3,0): 0->1, 1->2, 2->0, 2->3, 3->0, 0->2;
+      // lane k side k, lanes 0 and 1 also side 4 + k
+      auto side = [&](int j) {
+        const int a2 = j == 0 ? 0 : j == 1 ? 1 : j == 2 ? 2 : j == 3 ? 2 : j == 4 ? 3 : 0;
+        const int b2 = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j == 3 ? 3 : j == 4 ? 0 : 2;
+        return det_hypotf(qc[b2][0] - qc[a2][0], qc[b2][1] - qc[a2][1]);
+      };
+      const float s0 = side(k), s1 = side(4 + (k & 1));
+      float len[6];
+#pragma unroll
+      for (int j = 0; j < 4; j++) len[j] = fromf(s0, j);
+      len[4] = fromf(s1, 0);
+      len[5] = fromf(s1, 1);
+      float area = 0, pp;
+      pp = (len[0] + len[1] + len[2]) / 2;
+      area += sqrtf(pp * (pp - len[0]) * (pp - len[1]) * (pp - len[2]));
+      pp = (len[3] + len[4] + len[5]) / 2;
+      area += sqrtf(pp * (pp - len[3]) * (pp - len[4]) * (pp - len[5]));
+      if ((double)area < 0.95 * g.min_tag_width * g.min_tag_width) ok = false;
+    }
+    if (ok) {
+      const int i0 = k, i1 = (i0 + 1) & 3, i2 = (i0 + 2) & 3;
+      const float dx1 = qc[i1][0] - qc[i0][0], dy1 = qc[i1][1] - qc[i0][1];
+      const float dx2 = qc[i2][0] - qc[i1][0], dy2 = qc[i2][1] - qc[i1][1];
+      const float cosd = (dx1 * dx2 + dy1 * dy2) / sqrtf((dx1 * dx1 + dy1 * dy1) * (dx2 * dx2 + dy2 * dy2));
+      const int abad = (double)fabsf(cosd) > prm.cos_critical_rad || dx1 * dy2 < dy1 * dx2;
+      if (quad_or(abad)) ok = false;
+    }
+    if (k == 0) {
+      QuadRecord rec;
+      rec.blob_index = qp.blob_index;
+      rec.valid = valid;
+      for (int j = 0; j < 4; j++) rec.indices[j] = qp.indices[j];
+      QuadCand qcand;
+      for (int j = 0; j < 4; j++) {  // AdjustPixelCenters, quad_decimate 2
+        const float x = ok ? (qc[j][0] - 0.5f) * 2.0f + 0.5f : 0.f;
+        const float y = ok ? (qc[j][1] - 0.5f) * 2.0f + 0.5f : 0.f;
+        rec.corners[j][0] = qcand.p[j][0] = x;
+        rec.corners[j][1] = qcand.p[j][1] = y;
+      }
+      rec.accepted = ok;
+      b.quads[slot] = rec;
+      if (ok && !AT_DIAG_STOP(prm, 5)) {
+        qcand.frame = f;
+        qcand.rank = rank;
+        const uint32_t ci = atomicAdd(b.nqcand + (size_t)f * kQcStride, 1u);
+        if (ci < (uint32_t)kQuadCandPerFrame) b.qcand[(size_t)f * kQuadCandPerFrame + ci] = qcand;
+        else atomicOr(b.status + f, kStatusQuadsOverflow);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K9b: one accepted quad per 64-lane workgroup iteration (persistent):
 // RefineEdges with UnDistort/ReDistort (apriltag_detect.cu:405-564),
@@ -4490,7 +4619,7 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
 #pragma unroll
     for (int k = 0; k < kMaxBatch / 64; k++) {
       const int f = tid * (kMaxBatch / 64) + k;
-      c[k] = f < B ? min(b.nqcand[f], (uint32_t)kQuadCandPerFrame) : 0u;
+      c[k] = f < B ? min(b.nqcand[(size_t)f * kQcStride], (uint32_t)kQuadCandPerFrame) : 0u;
       sum += c[k];
     }
     const uint32_t incl = wave_incl_scan(sum, AddOp(), 0u);
@@ -5338,10 +5467,19 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     else hipLaunchKernelGGL(k_blob_small<false>, dim3(prm.sblob_wg ? prm.sblob_wg : nblobwg * 2), dim3(256), 0, s, b, g, prm, g.nlarge, kNumCls, 0);
     tk(8, s, 1);
   };
+  // the side fits of the blobs the throughput-mode (non-FUSE) blob kernels fitted:
+  // every class, or (latency mode above 4096-point blobs) the large classes only.  In
+  // the stage profile it counts with k_blob; the kernel timer's k_blob span leaves it out
+  const int fin_c1 = g.ctw != 32 ? kNumCls : g.max_cluster > 4096 ? g.nlarge : 0;
+  auto quad_fin = [&](hipStream_t s) {
+    if (fin_c1 > 0 && on(9) && (!AT_DIAG_ANY(prm) || AT_DIAG_STOP(prm, 5)))  // (a blob-phase cut leaves no side moments)
+      hipLaunchKernelGGL(k_quad_fin, dim3(std::max(1, std::min(2048, 8 * B))), dim3(256), 0, s, b, g, prm, 0, fin_c1);
+  };
   if (ev || !st2 || lat_fused) {
     blob_small(st);
     mark();
     blob_large(st);
+    quad_fin(st);
     mark();
   } else {
     hipError_t e;
@@ -5360,6 +5498,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
     }
     if ((e = hipEventRecord(join, st2))) return e;
     if ((e = hipStreamWaitEvent(st, join, 0))) return e;
+    quad_fin(st);
   }
   // latency mode: the pose inside k_decode (a second wave per workgroup) unless
   // stages or one kernel are timed (the control block then leaves with k_pose,
