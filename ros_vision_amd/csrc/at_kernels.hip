@@ -4652,22 +4652,43 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
   // kernels append only those)
   const uint32_t G = gridDim.x;
   uint32_t pose_seq = 0;  // (POSE) quads handed to the pose wave
-  for (uint32_t item = blockIdx.x; item < nq; item += G) {
-    int lo = 0, hi = B - 1;  // last frame whose prefix <= item
+  // the next item's queue entry (its corners on lanes 0-3) and frame address are
+  // loaded while this one is processed: an item's chain starts at its gray loads
+  struct ItemPre {
+    int f;
+    uint32_t rank;
+    float px, py;
+    const uint8_t* gsrc;
+  };
+  auto prefetch = [&](uint32_t it) -> ItemPre {
+    int lo = 0, hi = B - 1;  // last frame whose prefix <= it (the entry's frame)
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (qpre[mid] <= item) lo = mid;
+      if (qpre[mid] <= it) lo = mid;
       else hi = mid - 1;
     }
-    const QuadCand& qd = b.qcand[(size_t)lo * kQuadCandPerFrame + (item - qpre[lo])];
-    const int f = (int)qd.frame;
-    const uint32_t qrank = qd.rank;
+    const QuadCand* q = &b.qcand[(size_t)lo * kQuadCandPerFrame + (it - qpre[lo])];
+    ItemPre p;
+    p.f = lo;
+    p.rank = q->rank;
+    p.px = tid < 4 ? q->p[tid & 3][0] : 0.f;
+    p.py = tid < 4 ? q->p[tid & 3][1] : 0.f;
     // luma of pixel i = y W + x: the frame's own Y bytes for YUYV (every second byte)
     // and GRAY8 input, the gray plane k_pre wrote for BGR8
-    const uint8_t* gsrc = fmt == 1 ? b.gray + (size_t)f * g.W * g.H : b.frames[f];
+    p.gsrc = fmt == 1 ? b.gray + (size_t)lo * g.W * g.H : b.frames[lo];
+    return p;
+  };
+  ItemPre nxt = {};
+  if (blockIdx.x < nq) nxt = prefetch(blockIdx.x);
+  for (uint32_t item = blockIdx.x; item < nq; item += G) {
+    const ItemPre cur = nxt;
+    if (item + G < nq) nxt = prefetch(item + G);
+    const int f = cur.f;
+    const uint32_t qrank = cur.rank;
+    const uint8_t* gsrc = cur.gsrc;
     const int gsh = fmt == 0 ? 1 : 0;
     auto pix = [&](size_t i) -> uint32_t { return gsrc[i << gsh]; };
-    if (tid < 4) { S.qc[tid][0] = qd.p[tid][0]; S.qc[tid][1] = qd.p[tid][1]; }
+    if (tid < 4) { S.qc[tid][0] = cur.px; S.qc[tid][1] = cur.py; }
     team_sync<64>();
     phase(0);
     if (prm.refine_edges) {
@@ -4969,8 +4990,8 @@ __global__ __launch_bounds__(POSE ? 128 : kDecodeThreads) __attribute__((amdgpu_
       // the codebook straight from HBM (L2-resident: every workgroup reads the same
       // table; an LDS copy cost 8 KB per one-wave workgroup, and the LDS freed lets
       // the concurrent batches' kernels co-reside: +2.8 % throughput, profiles/r03l),
-      // four of a lane's entries loaded together (tag36h11: 3 round trips instead of 10)
-      constexpr int kBookChunk = 4;
+      // ten of a lane's entries loaded together (tag36h11: one round trip instead of 10)
+      constexpr int kBookChunk = 10;  // (every family in one round trip: ncodes <= 640)
       for (int e0 = 0; e0 < prm.fam.ncodes; e0 += kBookChunk * kDecodeThreads) {
         uint64_t cw[kBookChunk];
 #pragma unroll
