@@ -172,14 +172,23 @@ __device__ __forceinline__ void polar_rank2_cols(const V3& m0, const V3& m1, V3&
   }
 }
 
+// (one reciprocal instead of nine divisions: within the pose tolerance, like the
+// contracted products above)
 __device__ __forceinline__ M3 calculate_F(const V3& v) {
   M3 F;
-  const double inner = v_dot(v, v);
+  const double ri = 1.0 / v_dot(v, v);
 #pragma unroll
   for (int i = 0; i < 3; i++)
 #pragma unroll
-    for (int j = 0; j < 3; j++) F.m[i][j] = v.v[i] * v.v[j] / inner;
+    for (int j = 0; j < 3; j++) F.m[i][j] = v.v[i] * v.v[j] * ri;
   return F;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
 }
 
 // orthogonal_iteration over the 4 tag corners p_j = (sx_j, sy_j, 0).
@@ -192,6 +201,10 @@ __device__ __forceinline__ M3 calculate_F(const V3& v) {
 // (sum_j sx_j = sum_j sy_j = 0 removes the I and q_mean terms).  The step is
 // then R <- polar(M3).  As upstream, the returned t belongs to the R before the last step
 // and the error to the final (R, t).
+// WAVE (a whole wave per detection): lane c < 6 evaluates component c of (m0, m1) -- the
+// same balanced 6-term dot product -- and every lane reads the six back, so a step issues
+// one dot product and six lane reads instead of six dot products.
+template <bool WAVE = false>
 __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, int n_steps, int* steps = nullptr) {
   M3 Gx, Gy, Fs, Fxy;
   {
@@ -250,14 +263,36 @@ __device__ double orthogonal_iteration(const V3* v, const V3* p, V3* t, M3* R, i
   // whose t upstream returns
   V3 r0 = {{R->m[0][0], R->m[1][0], R->m[2][0]}}, r1 = {{R->m[0][1], R->m[1][1], R->m[2][1]}};
   V3 q0 = r0, q1 = r1;
+  // (WAVE) this lane's row of [A00 A01; A10 A11]: component c = lane % 6 of (m0, m1)
+  double cr[6];
+  if constexpr (WAVE) {
+    const int c = (int)(__lane_id() % 6), i = c % 3;
+    const M3& L = c < 3 ? A00 : A10;
+    const M3& Rm = c < 3 ? A01 : A11;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      cr[j] = L.m[i][j];
+      cr[3 + j] = Rm.m[i][j];
+    }
+  }
   auto step = [&](const V3& x0, const V3& x1, V3& y0, V3& y1) {
     V3 m0, m1;
+    if constexpr (WAVE) {
+      const double mine = ((cr[0] * x0.v[0] + cr[1] * x0.v[1]) + (cr[2] * x0.v[2] + cr[3] * x1.v[0])) +
+                          (cr[4] * x1.v[1] + cr[5] * x1.v[2]);
 #pragma unroll
-    for (int i = 0; i < 3; i++) {  // balanced 6-term dot products
-      m0.v[i] = ((A00.m[i][0] * x0.v[0] + A00.m[i][1] * x0.v[1]) + (A00.m[i][2] * x0.v[2] + A01.m[i][0] * x1.v[0])) +
-                (A01.m[i][1] * x1.v[1] + A01.m[i][2] * x1.v[2]);
-      m1.v[i] = ((A10.m[i][0] * x0.v[0] + A10.m[i][1] * x0.v[1]) + (A10.m[i][2] * x0.v[2] + A11.m[i][0] * x1.v[0])) +
-                (A11.m[i][1] * x1.v[1] + A11.m[i][2] * x1.v[2]);
+      for (int i = 0; i < 3; i++) {
+        m0.v[i] = readlane_f64(mine, i);
+        m1.v[i] = readlane_f64(mine, 3 + i);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; i++) {  // balanced 6-term dot products
+        m0.v[i] = ((A00.m[i][0] * x0.v[0] + A00.m[i][1] * x0.v[1]) + (A00.m[i][2] * x0.v[2] + A01.m[i][0] * x1.v[0])) +
+                  (A01.m[i][1] * x1.v[1] + A01.m[i][2] * x1.v[2]);
+        m1.v[i] = ((A10.m[i][0] * x0.v[0] + A10.m[i][1] * x0.v[1]) + (A10.m[i][2] * x0.v[2] + A11.m[i][0] * x1.v[0])) +
+                  (A11.m[i][1] * x1.v[1] + A11.m[i][2] * x1.v[2]);
+      }
     }
     polar_rank2_cols(m0, m1, y0, y1);
   };
@@ -491,12 +526,6 @@ __device__ __forceinline__ void solve_poly_level_wave_lane(const double* p, int 
     }
   }
 }
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-  return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
-}
 __device__ __forceinline__ int solve_poly_level_wave(const double* p, int degree, const double* der_roots, int n_der, double* roots) {
   double my_root;
   int my_has;
@@ -726,14 +755,14 @@ __device__ void estimate_tag_pose(const double H[9], const double corners[4][2],
     R1.m[2][c] = -R1.m[2][c];
   }
   int k1 = 0, k2 = 0;
-  const double err1 = orthogonal_iteration(v, p, &t1, &R1, 50, &k1);
+  const double err1 = orthogonal_iteration<WAVE>(v, p, &t1, &R1, 50, &k1);
   if (stamps) stamps[2] = wall_clock64();
   M3 R2;
   V3 t2 = {{0, 0, 0}};
   double err2 = HUGE_VAL;
   const bool amb = fix_pose_ambiguities<WAVE>(v, p, t1, R1, &R2, sub, stamps);
   if (stamps) stamps[3] = wall_clock64();
-  if (amb) err2 = orthogonal_iteration(v, p, &t2, &R2, 50, &k2);
+  if (amb) err2 = orthogonal_iteration<WAVE>(v, p, &t2, &R2, 50, &k2);
   if (stamps) {
     stamps[4] = wall_clock64();
     stamps[8] = k1;

@@ -10,6 +10,7 @@
 #                      FETCH / WRITE passes (pmc_traffic_1080p.json)
 #   BENCH=1            the default bench line -> bench.json
 #   BSTOPS="0 2 3 4 7 8"  blob kernels cut after a phase (experiment build): serialized stage ms
+#   LATLIBS="a b"      B = 1 latency (p50 / p99 from HBM) of each library, three interleaved rounds
 #   LIBS="a.so b.so"   interleaved concurrent A/B at 720p (tools/ab_stages.sh)
 #   LIBS1080="a b"     the same at 1080p
 #   PMCLIBS="a b"      FETCH / WRITE bytes per kernel of each library (tools/pmc_ab.sh)
@@ -53,6 +54,14 @@ if [ -n "${BSTOPS:-}" ]; then  # blob kernels cut after phase N (AT_DIAG_BLOB_ST
     AT_HIP_LIB=$EXP AT_DIAG_BLOB_STOP=$st timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --latency-frames 0 \
       --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --no-kernel-timer 2>>$O/err.txt | python3 -c "
 import json,sys; j=json.load(sys.stdin); s=j['stage_ms_per_batch']; print(j['value'], 'k_blob_small=%.4f k_blob=%.4f k_decode=%.4f' % (s['k_blob_small'], s['k_blob'], s['k_decode']))" >> $O/blob_stops.txt || exit 1
+  done; done
+fi
+if [ -n "${LATLIBS:-}" ]; then  # B = 1 latency of each library, interleaved rounds
+  for r in 1 2 3; do for lib in $LATLIBS; do
+    echo -n "round=$r lib=$lib " >> $O/lat.txt
+    AT_HIP_LIB=$lib timeout -k 10 200 python3 bench.py --steps 3 --warmup 2 --latency-frames ${LATN:-2000} --no-cpu-baseline --no-stage-profile \
+      --no-kernel-timer --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --isolated-batches 0 2>>$O/err.txt | python3 -c "
+import json,sys; j=json.load(sys.stdin); print('p50 %.4f p99 %.4f' % (j['p50_latency_hbm_ms'], j['p99_latency_hbm_ms']))" >> $O/lat.txt || exit 1
   done; done
 fi
 if [ -n "${LIBS:-}" ]; then TAG=$TAG bash tools/ab_stages.sh > /dev/null || exit 1; fi
