@@ -152,7 +152,8 @@ long long at_debug_copy(at_detector *d, int stage, int frame, void *dst, size_t 
  * back (8 B per point of every selected blob): off by default (production), on
  * with at_set_debug_taps(d, 1) for parity checks; AT_E_INVALID while off.
  * AT_STAGE_SIZES of a throughput-mode batch (max_batch >= 8) likewise needs the taps
- * (that mode carries the size test in the root words, not in the size plane). */
+ * (that mode carries the size test in the root words, not in the size plane), and so
+ * does AT_STAGE_QUADS (the fitted-quad records are debug output only). */
 int at_set_debug_taps(at_detector *d, int enable);
 
 /* Fitted quad record (FitQuad + QuadCorners, line_fit_filter.h:130-135 and

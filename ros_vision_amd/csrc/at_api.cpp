@@ -1252,7 +1252,9 @@ long long at_debug_copy(at_detector* d, int stage, int frame, void* dst, size_t 
       return 4;
     case AT_STAGE_PROBE: src = d->d.probe; n = kProbeWords * 8; break;
     case AT_STAGE_QUADS: {
-      // one record per kept blob, in the slot of its pair rank (pair_sel marks them)
+      // one record per kept blob, in the slot of its pair rank (pair_sel marks them),
+      // written while the debug taps are on
+      if (!d->prm.taps) return AT_E_INVALID;
       const uint32_t npairs = std::min<uint32_t>(d->h_ctrl[kCtlNpairs * B + frame], (uint32_t)kMaxPairs);
       std::vector<QuadRecord> all(npairs);
       std::vector<uint32_t> sel(npairs);

@@ -228,15 +228,17 @@ struct Moments {
   int32_t N;
 };
 
-// A kept blob's side fits left to k_quad_fin (throughput mode): the moments of the
-// four side segments of its best combination, and the record's fields.  The blob's
-// wave writes them (lanes 0-3 a segment each); k_quad_fin fits the four lines, the
-// corners and the Heron / angle tests with a thread per blob.
+// A kept blob's side fits left to k_quad_fin (throughput mode): per side segment of its
+// best combination, FitLine's (float)(Cxx - Cyy), (float)(2 Cxy) and centroid quotients
+// (all the corners need of the fit), and the record's fields.  The blob's team writes
+// them (threads 0-3 a segment each); k_quad_fin finishes the four lines, the corners
+// and the Heron / angle tests.
 struct QuadPend {
-  Moments seg[4];
+  float fit[4][4];
   uint32_t blob_index, valid;
   uint16_t indices[4];
 };
+static_assert(sizeof(QuadPend) == 80, "QuadPend: 80 B per kept blob");
 
 // One 2-px-thick segment of the annotated image (at_draw_outlines_device).
 struct DrawPrim {

@@ -2397,30 +2397,43 @@ __device__ __forceinline__ int32_t lf_weight(int32_t gx, int32_t gy) {
   return (int32_t)r + 1;
 }
 
-// FitLine (line_fit_filter.cu:798-872) / HostFitLine (apriltag_detect.cu:38-90)
-__device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* err, double* mse) {
+// FitLine's line normal (line_fit_filter.cu:798-872) from d = (float)(Cxx - Cyy),
+// c = (float)(2 Cxy) and h = hypot(d, c); (float)(Cyy - Cxx) is -d exactly (the int64 ->
+// float conversion rounds symmetrically)
+__device__ __forceinline__ void line_normal(float d, float c, float h, double* lp23) {
+  const float nx1 = d - h, ny1 = c;
+  const float M1 = nx1 * nx1 + ny1 * ny1;
+  const float nx2 = c, ny2 = -d - h;
+  const float M2 = nx2 * nx2 + ny2 * ny2;
+  float nx, ny;
+  if (M1 > M2) { nx = nx1; ny = ny1; } else { nx = nx2; ny = ny2; }
+  const float len = det_hypotf(nx, ny);
+  lp23[0] = (double)(nx / len);
+  lp23[1] = (double)(ny / len);
+}
+
+// FitLine (line_fit_filter.cu:798-872) / HostFitLine (apriltag_detect.cu:38-90).
+// pre (optional): d, c and the centroid quotients, which are all UpdateFitQuads'
+// corners need of the fit (k_quad_fin finishes from them)
+__device__ void fit_line(const Moments& m, double* lp01, double* lp23, double* err, double* mse, float* pre = nullptr) {
   const int64_t W = m.W;
   const int64_t Cxx = (int64_t)((uint64_t)m.Mxx * (uint64_t)W - (uint64_t)((int64_t)m.Mx * (int64_t)m.Mx));
   const int64_t Cxy = (int64_t)((uint64_t)m.Mxy * (uint64_t)W - (uint64_t)((int64_t)m.Mx * (int64_t)m.My));
   const int64_t Cyy = (int64_t)((uint64_t)m.Myy * (uint64_t)W - (uint64_t)((int64_t)m.My * (int64_t)m.My));
-  const float h = det_hypotf((float)(Cxx - Cyy), (float)(2 * Cxy));
+  const float d = (float)(Cxx - Cyy), c = (float)(2 * Cxy);
+  const float px = (float)m.Mx / (float)(m.W * 2), py = (float)m.My / (float)(m.W * 2);
+  if (pre) {
+    pre[0] = d; pre[1] = c; pre[2] = px; pre[3] = py;
+    return;
+  }
+  const float h = det_hypotf(d, c);
   const float e8 = (float)((double)(W * W) * 8.0);
   const float eig = ((float)(Cxx + Cyy) - h) / e8;
   if (lp01) {
-    lp01[0] = (double)((float)m.Mx / (float)(m.W * 2));
-    lp01[1] = (double)((float)m.My / (float)(m.W * 2));
+    lp01[0] = (double)px;
+    lp01[1] = (double)py;
   }
-  if (lp23) {
-    const float nx1 = (float)(Cxx - Cyy) - h, ny1 = (float)(2 * Cxy);
-    const float M1 = nx1 * nx1 + ny1 * ny1;
-    const float nx2 = (float)(2 * Cxy), ny2 = (float)(Cyy - Cxx) - h;
-    const float M2 = nx2 * nx2 + ny2 * ny2;
-    float nx, ny;
-    if (M1 > M2) { nx = nx1; ny = ny1; } else { nx = nx2; ny = ny2; }
-    const float len = det_hypotf(nx, ny);
-    lp23[0] = (double)(nx / len);
-    lp23[1] = (double)(ny / len);
-  }
+  if (lp23) line_normal(d, c, h, lp23);
   *err = (double)((float)m.N * eig);
   *mse = (double)eig;
 }
@@ -3813,7 +3826,13 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
     // throughput mode: the side segments' moments for k_quad_fin (a thread per blob
     // there, instead of a few lanes of this team on a serial fp64 chain here)
     QuadPend& qp = b.qpend[(size_t)f * kMaxPairs + rank];
-    if (valid && tid < 4) qp.seg[tid] = seg_moments((cbt >> (8 * tid)) & 0xff, (cbt >> (8 * ((tid + 1) & 3))) & 0xff);
+    if (valid && tid < 4) {
+      float pre[4];
+      double e_, m_;
+      fit_line(seg_moments((cbt >> (8 * tid)) & 0xff, (cbt >> (8 * ((tid + 1) & 3))) & 0xff), nullptr, nullptr, &e_, &m_,
+               pre);
+      *reinterpret_cast<float4*>(qp.fit[tid]) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+    }
     if (tid == 0) {
       qp.blob_index = bi;
       qp.valid = valid;
@@ -3911,7 +3930,7 @@ __device__ void blob_item(const DevBufs& b, const Geom& g, const Params& prm, Bl
       rec.corners[k][1] = qcand.p[k][1] = y;
     }
     rec.accepted = ok;
-    b.quads[(size_t)f * kMaxPairs + rank] = rec;  // slot = pair rank: no returning atomic
+    if (prm.taps) b.quads[(size_t)f * kMaxPairs + rank] = rec;  // slot = pair rank (debug record: taps only)
     pacc[21] += 1;  // FitQuads records of this team (batch statistics, one atomic per team at the end)
     if (ok && !AT_DIAG_STOP(prm, 5)) {
       qcand.frame = (uint32_t)f;
@@ -4362,9 +4381,11 @@ __global__ __launch_bounds__(256) void k_quad_fin(DevBufs b, Geom g, Params prm,
     int bad = 0;
     {
       double l[4] = {0, 0, 0, 0};
-      if (valid) {
-        const LineFitOut o = fit_line_v<true, true>(qp.seg[k]);
-        l[0] = o.p01[0]; l[1] = o.p01[1]; l[2] = o.p23[0]; l[3] = o.p23[1];
+      if (valid) {  // fit_line's p01 and p23 from the blob team's d, c and centroid
+        const float4 pre = *reinterpret_cast<const float4*>(qp.fit[k]);
+        l[0] = (double)pre.z;
+        l[1] = (double)pre.w;
+        line_normal(pre.x, pre.y, det_hypotf(pre.x, pre.y), l + 2);
       }
       double m[4];
 #pragma unroll
@@ -4434,7 +4455,7 @@ __global__ __launch_bounds__(256) void k_quad_fin(DevBufs b, Geom g, Params prm,
         rec.corners[j][1] = qcand.p[j][1] = y;
       }
       rec.accepted = ok;
-      b.quads[slot] = rec;
+      if (prm.taps) b.quads[slot] = rec;  // (debug record: AT_STAGE_QUADS with the taps on)
       if (ok && !AT_DIAG_STOP(prm, 5)) {
         qcand.frame = f;
         qcand.rank = rank;
