@@ -363,6 +363,7 @@ int at_create(const at_config* cfg, const at_camera* cam, at_detector** out) {
   p.pipe_stop = knob_int("AT_DIAG_PIPE_STOP", 0);
   p.lblob_wg = knob("AT_LBLOB_WG") ? std::max(16, knob_int("AT_LBLOB_WG", 0)) : 0;  // experiment
   p.sblob_wg = knob("AT_SBLOB_WG") ? std::max(16, knob_int("AT_SBLOB_WG", 0)) : 0;  // experiment
+  p.dec_wg = knob("AT_DEC_WG") ? std::max(16, knob_int("AT_DEC_WG", 0)) : 0;  // experiment
   p.fam = family_desc(*fam);
   d->use_graphs = !knob_int("AT_NO_GRAPH", 0);
   if (!(cfg->tag_size >= 0) || !std::isfinite(cfg->tag_size)) {

@@ -159,6 +159,7 @@ struct Params {
   int pipe_stop;  // diagnostics only (AT_DIAG_PIPE_STOP): launch the stages < N only; 0 = all
   int lblob_wg;   // throughput-mode large-blob kernel's persistent grid (AT_LBLOB_WG; 0: nblobwg)
   int sblob_wg;   // small-blob kernel's persistent grid (AT_SBLOB_WG; 0: 2 nblobwg)
+  int dec_wg;     // k_decode's persistent grid (AT_DEC_WG, experiment; 0: decode_grid)
   FamilyDesc fam;
   int gp_w, gp_h, gp_c;  // game-piece preprocessing output (at_gp_enable); gp_c == 0: off
 };

@@ -2993,7 +2993,8 @@ constexpr uint32_t kRegSortMaxBucket = 512;
 // false with the keys in S.keys in load order when a bucket exceeds 32 keys.
 template <int CAP>
 __device__ bool wave_bucket_sort_kv(BlobShared<64, CAP>& S, uint64_t (&kv)[CAP / 64], int n) {
-  static_assert(CAP % 64 == 0 && CAP <= 512, "wave sort: at most 8 keys per lane");
+  static_assert(CAP % 64 == 0 && CAP <= 1024, "wave sort: at most 16 keys per lane");
+  constexpr int PB = CAP > 512 ? 8 : 4;  // buckets per lane at most (nb < n <= CAP: nb <= CAP / 2)
   static_assert(kThetaSpan <= (1ull << 26), "theta fits 26 bits");
   constexpr int KPL = CAP / 64;
   const uint32_t lane = lane_id();
@@ -3015,9 +3016,9 @@ __device__ bool wave_bucket_sort_kv(BlobShared<64, CAP>& S, uint64_t (&kv)[CAP /
   // exclusive scan of the nb counts, each lane owning nb/64 (or one) consecutive buckets
   const int per = nb >= 64 ? nb / 64 : 1;
   const int b0 = (int)lane * per;
-  uint32_t cval[4], loc = 0, mx = 0;
+  uint32_t cval[PB], loc = 0, mx = 0;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < PB; j++) {
     cval[j] = 0;
     if (j < per && b0 + j < nb) {
       const uint32_t bb = (uint32_t)(b0 + j);
@@ -3040,15 +3041,15 @@ __device__ bool wave_bucket_sort_kv(BlobShared<64, CAP>& S, uint64_t (&kv)[CAP /
   team_sync<64>();
   // bucket starts in place (u16 each)
   uint32_t run = incl - loc;
-  uint32_t st[4];
+  uint32_t st[PB];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < PB; j++) {
     st[j] = run;
     if (j < per && b0 + j < nb) run += cval[j];
   }
   if (per >= 2) {
 #pragma unroll
-    for (int j = 0; j < 4; j += 2)
+    for (int j = 0; j < PB; j += 2)
       if (j < per) bcnt[(b0 + j) >> 1] = st[j] | (st[j + 1] << 16);
   } else if (b0 < nb) {  // one bucket per lane: the even lane writes both halves of the word
     const uint32_t other = wave_read_next(st[0]);
@@ -4290,19 +4291,23 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
 #define AT_BS_WAVES 4
 #endif
 
-// Classes c0 .. c1-1 of blobs of up to CAP points; `launch` > 0: not the stage's first
-// launch (appends its device-clock stamps).  (A CAP-128 launch for the blobs of up to
-// 128 points kept 123 VGPRs -- the per-blob fits, not the per-point arrays, set the
-// register count -- so the small blobs stay in one CAP-512 launch.)
-template <bool FUSE, int CAP = kSmallBlob, int WAVES = AT_BS_WAVES>
+// Classes c0 .. c1-1 of blobs of up to CAP points, timed as stage STAGE; `launch` > 0:
+// not the stage's first launch (appends its device-clock stamps).  (A CAP-128 launch for
+// the blobs of up to 128 points kept 123 VGPRs -- the per-blob fits, not the per-point
+// arrays, set the register count -- so the small blobs stay in one CAP-512 launch.)
+// Throughput mode also runs the 513-1024-point class this way (CAP 1024, 16 keys per
+// lane, 188 VGPRs: 2 waves per SIMD) as the large-blob stage's second launch: one wave
+// per blob and no workgroup barriers, where 128-thread teams spent 63 % of their
+// wave-cycles waiting (+1.7 % frames/s, profiles/r06/ab720_mid_wave_stages.txt).
+template <bool FUSE, int CAP = kSmallBlob, int WAVES = AT_BS_WAVES, int STAGE = 8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : WAVES))) void k_blob_small(DevBufs b, Geom g, Params prm,
                                                                                                          int c0, int c1, int launch) {
   __shared__ BlobShared<64, CAP> Ss[4];
   const int wave = threadIdx.x >> 6;
   uint32_t kt_slot = ~0u;
   if (!launch) {
-    kt_begin(b, 8);
-  } else if (b.kt_stage == 8 && threadIdx.x == 0) {
+    kt_begin(b, STAGE);
+  } else if (b.kt_stage == STAGE && threadIdx.x == 0) {
     kt_slot = atomicAdd(b.kgrid, 1u);
     if (kt_slot < b.kwg_cap) b.kwg[kt_slot] = wall_clock64();
   }
@@ -4311,9 +4316,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FUSE ? 2 : 
   if (threadIdx.x < kNumCls) s_cnt[threadIdx.x] = min(b.ncls[threadIdx.x], b.wcap);
   __syncthreads();
   small_blob_loop<FUSE, CAP>(b, g, prm, Ss[wave], s_combo, s_cnt, blockIdx.x * 4 + wave, gridDim.x * 4, c0, c1);
-  if (b.kt_stage == 8) {  // (uniform: the timed launch only)
+  if (b.kt_stage == STAGE) {  // (uniform: the timed launch only)
     __syncthreads();
-    if (threadIdx.x == 0 && !launch) kt_end(b, 8);
+    if (threadIdx.x == 0 && !launch) kt_end(b, STAGE);
     if (threadIdx.x == 0 && launch && kt_slot < b.kwg_cap) b.kwg[b.kwg_cap + kt_slot] = wall_clock64();
   }
 }
@@ -5487,15 +5492,16 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
       else hipLaunchKernelGGL((k_blob<512, kSortCap>), dim3(nblobwg), dim3(512), 0, s, b, g, prm, 0u, 0, g.nlarge, 0);
     } else {
       // throughput: blobs of 1025-4096 points (size classes 0 .. nlarge-2) in 256-thread
-      // teams, the 513-1024-point class (nlarge-1: two thirds of the large blobs) in
-      // 128-thread teams (CAP 1024: the same 8 points per thread as the one-wave kernel;
-      // barriers over two waves); geometries whose blobs exceed 4096 points (1080p) add a
+      // teams, the 513-1024-point class (nlarge-1: two thirds of the large blobs) one
+      // wave per blob (k_blob_small at CAP 1024: 16 points per lane, no workgroup
+      // barriers; round 6's 128-thread teams waited at them 63 % of their wave-cycles);
+      // geometries whose blobs exceed 4096 points (1080p) add a
       // launch of CAP-8192 teams over those (class 0 above 4096), AT_BIG_NT threads each:
       // 16 keys per thread keep its theta sort in registers (256-thread teams held 32 and
       // fell back to a bitonic sort of 8192 keys)
       const int lo = prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg;
       hipLaunchKernelGGL((k_blob<256, 4096>), dim3(lo), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge - 1, 0);
-      hipLaunchKernelGGL((k_blob<128, 1024>), dim3(2 * nblobwg), dim3(128), 0, s, b, g, prm, 0u, g.nlarge - 1, g.nlarge, 1);
+      hipLaunchKernelGGL((k_blob_small<false, 1024, 2, 9>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, g.nlarge - 1, g.nlarge, 1);
       if (!cap4k)
         hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g,
                            prm, 4096u, 0, 1, 2);
@@ -5550,7 +5556,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups
     // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
-    const dim3 grd(decode_grid(nblobwg, B));
+    const dim3 grd(prm.dec_wg ? prm.dec_wg : decode_grid(nblobwg, B));
     if (on(10) && pose_fused) hipLaunchKernelGGL(k_decode<true>, grd, dim3(128), 0, st, b, g, prm, B, fmt);
     else if (on(10)) hipLaunchKernelGGL(k_decode<false>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B, fmt);
   }

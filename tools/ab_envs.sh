@@ -11,7 +11,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   if [ $((r % 2)) = 0 ]; then ORDER=$REV; fi
   for ev in $ORDER; do
     env AT_HIP_LIB=${AT_HIP_LIB:-ros_vision_amd/ab/libat_hip_exp.so} $ev timeout -k 10 150 python3 bench.py --steps ${STEPS:-100} --warmup 5 --no-cpu-baseline \
-      --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 --no-kernel-timer --pool 128 \
+      --latency-frames 0 --host-ingest-steps 0 --c3-latency-iters 0 --node-path-calls 0 --no-kernel-timer --pool 128 \
       2>>$OUT/err.txt | python3 -c "
 import json,sys; j=json.load(sys.stdin)
 print('round=$r lib=$ev', j['value'], j['p50_latency_hbm_ms'], ' '.join('%s=%.4f' % kv for kv in j['stage_ms_per_batch'].items()))" >> $OUT/stages.txt || exit 1

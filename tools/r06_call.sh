@@ -13,6 +13,7 @@
 #   LATLIBS="a b"      B = 1 latency (p50 / p99 from HBM) of each library, three interleaved rounds
 #   LIBS="a.so b.so"   interleaved concurrent A/B at 720p (tools/ab_stages.sh)
 #   LIBS1080="a b"     the same at 1080p
+#   ENVS="AT_X=1 AT_X=2"  interleaved A/B of experiment-build knobs (tools/ab_envs.sh)
 #   PMCLIBS="a b"      FETCH / WRITE bytes per kernel of each library (tools/pmc_ab.sh)
 #   ISO=1              bench.py --isolated-only under rocprofv3 --kernel-trace --stats
 set -o pipefail
@@ -65,6 +66,7 @@ import json,sys; j=json.load(sys.stdin); print('p50 %.4f p99 %.4f' % (j['p50_lat
   done; done
 fi
 if [ -n "${LIBS:-}" ]; then TAG=$TAG bash tools/ab_stages.sh > /dev/null || exit 1; fi
+if [ -n "${ENVS:-}" ]; then TAG=$TAG bash tools/ab_envs.sh > /dev/null || exit 1; fi
 if [ -n "${LIBS1080:-}" ]; then
   for r in 1 2; do for lib in $LIBS1080; do
     echo -n "round=$r lib=$lib " >> $O/ab1080.txt
