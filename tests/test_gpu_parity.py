@@ -582,3 +582,23 @@ def test_ccl_adversarial_unions(gpu, oracle_mod):
         assert np.array_equal(det.copy_union_markers_size(j), want[j % 8][1]), j
     for j in range(8):
         assert compare_frame(det, orcs[j], frame_idx=j) == [], j
+
+
+@pytest.mark.parametrize("batch", [1, 8])
+def test_debug_records_need_the_taps(batch):
+    """The fitted-quad records (AT_STAGE_QUADS) are debug output the blob kernels and
+    k_quad_fin write only while the taps are on: without them the copy is refused
+    (AT_E_INVALID), never served stale; with them every detection has its accepted quad."""
+    import ros_vision_amd as rva
+    from ros_vision_amd import synth
+    frame = synth.stream_frame(1280, 720, 2)[0]
+    det = rva.GpuDetector(1280, 720, max_batch=batch, debug_taps=False)
+    det.detect_batch([frame])
+    with pytest.raises(RuntimeError):
+        det.copy_quads(0)
+    det.close()
+    det = rva.GpuDetector(1280, 720, max_batch=batch, debug_taps=True)
+    res = det.detect_batch([frame])
+    quads = det.copy_quads(0)
+    assert len(res[0]) > 0 and sum(q["accepted"] for q in quads) >= len(res[0])
+    det.close()
