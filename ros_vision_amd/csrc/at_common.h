@@ -69,7 +69,10 @@ constexpr int kNMaxima = 10;
 // RefineEdges samples of one quad (<= perimeter / 8 + 64, k_decode): the first
 // kLdsRefine in LDS, the rest in the decode workgroup's global scratch
 constexpr int kMaxRefineSamples = 1536;
-constexpr int kLdsRefine = 256;
+#ifndef AT_LDS_REFINE
+#define AT_LDS_REFINE 256
+#endif
+constexpr int kLdsRefine = AT_LDS_REFINE;
 constexpr int kDecodeGridPerBlobWg = 8;  // k_decode workgroups <= nblobwg * this
 // k_decode's persistent grid for a batch of B frames: enough one-wave groups for
 // every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)

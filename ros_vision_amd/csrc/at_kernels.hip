@@ -5556,7 +5556,8 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
   {
     // one wave per workgroup, persistent over the accepted quads: enough groups
     // for every quad of a full batch to start at once (16 per CU at 8.5 KB LDS)
-    const dim3 grd(prm.dec_wg ? prm.dec_wg : decode_grid(nblobwg, B));
+    // (the experiment knob never exceeds the grid the refine scratch was sized for)
+    const dim3 grd(prm.dec_wg ? std::min(prm.dec_wg, decode_grid(nblobwg, B)) : decode_grid(nblobwg, B));
     if (on(10) && pose_fused) hipLaunchKernelGGL(k_decode<true>, grd, dim3(128), 0, st, b, g, prm, B, fmt);
     else if (on(10)) hipLaunchKernelGGL(k_decode<false>, grd, dim3(kDecodeThreads), 0, st, b, g, prm, B, fmt);
   }
