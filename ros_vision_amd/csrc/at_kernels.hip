@@ -4296,7 +4296,8 @@ __global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint
 // the blobs of up to 128 points kept 123 VGPRs -- the per-blob fits, not the per-point
 // arrays, set the register count -- so the small blobs stay in one CAP-512 launch.)
 // Throughput mode also runs the 513-1024-point class this way (CAP 1024, 16 keys per
-// lane, 188 VGPRs: 2 waves per SIMD) as the large-blob stage's second launch: one wave
+// lane, 168 VGPRs: 3 waves per SIMD, +0.7 % over 2 at 188 VGPRs in three interleaved
+// rounds, profiles/r06/ab720_mid_wave3_stages.txt) as the large-blob stage's second launch: one wave
 // per blob and no workgroup barriers, where 128-thread teams spent 63 % of their
 // wave-cycles waiting (+1.7 % frames/s, profiles/r06/ab720_mid_wave_stages.txt).
 template <bool FUSE, int CAP = kSmallBlob, int WAVES = AT_BS_WAVES, int STAGE = 8>
@@ -5501,7 +5502,7 @@ hipError_t launch_pipeline(const DevBufs& b, const Geom& g, const Params& prm, i
       // fell back to a bitonic sort of 8192 keys)
       const int lo = prm.lblob_wg ? std::min(prm.lblob_wg, nblobwg) : nblobwg;
       hipLaunchKernelGGL((k_blob<256, 4096>), dim3(lo), dim3(256), 0, s, b, g, prm, 0u, 0, g.nlarge - 1, 0);
-      hipLaunchKernelGGL((k_blob_small<false, 1024, 2, 9>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, g.nlarge - 1, g.nlarge, 1);
+      hipLaunchKernelGGL((k_blob_small<false, 1024, 3, 9>), dim3(nblobwg), dim3(256), 0, s, b, g, prm, g.nlarge - 1, g.nlarge, 1);
       if (!cap4k)
         hipLaunchKernelGGL((k_blob<AT_BIG_NT, kSortCap>), dim3(std::min(nblobwg, AT_BIG_BLOB_WG)), dim3(AT_BIG_NT), 0, s, b, g,
                            prm, 4096u, 0, 1, 2);
