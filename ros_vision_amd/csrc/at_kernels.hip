@@ -4262,7 +4262,9 @@ __device__ __forceinline__ void small_blob_loop(const DevBufs& b, const Geom& g,
 // sorted by a bitonic fallback: k_blob 1.68 -> 0.68 ms per 192 frames, 1080p 45.8 k
 // -> 53.0 k frames/s, profiles/r06/ab1080_big_blob_teams.txt.)
 template <int NT, int CAP, bool FUSE = false>
-__global__ __launch_bounds__(NT) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo, int c0, int c1, int launch) {
+// (the throughput-mode 256-thread CAP-4096 teams at 3 waves per SIMD: 166 VGPRs, no
+// spills; +0.7 % over 2 waves in four interleaved rounds, profiles/r06/ab720_large_waves3.txt)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 && CAP == 4096 && !FUSE ? 3 : 1))) void k_blob(DevBufs b, Geom g, Params prm, uint32_t nlo, int c0, int c1, int launch) {
   __shared__ BlobShared<NT, CAP> S;
   const int tid = threadIdx.x;
   // device-clock span: the first launch's workgroups stamp their slots as usual; the
