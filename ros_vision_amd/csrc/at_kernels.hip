@@ -4124,7 +4124,9 @@ __device__ __forceinline__ void extents_item(const DevBufs& b, const Geom& g, ui
                         // scratch traffic per frame (profiles/r06/pmc_ext_ab.txt); 93 VGPRs fit 5
 #endif
 #ifndef AT_EXT_GRID
-#define AT_EXT_GRID 1536  // workgroups (persistent over the candidates): AT_EXT_WAVES x 256 CUs / 4
+#define AT_EXT_GRID 2560  // workgroups (persistent over the candidates): two full rounds of the 1280 the chip holds at 5 waves per SIMD
+                          // (1536 left a partial second round: 0.177 -> 0.160 ms serialized, concurrent
+                          // throughput unchanged, profiles/r06/ab720_extents_grid.txt)
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(AT_EXT_WAVES))) void k_extents(DevBufs b, Geom g) {
   __shared__ int64_t s_red[4][8];
